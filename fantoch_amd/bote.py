@@ -1,0 +1,522 @@
+"""`Bote`, `Search` and the streaming GPU sweep.
+
+Mirror of the `fantoch_bote` crate surface (reference `fantoch_bote/src/lib.rs`
+and `search.rs`) on top of the C ABI in include/bote_hip.h.  Every latency,
+quorum, leader choice, histogram moment, score and top-K selection is computed
+by the gfx950 kernels in libbote_hip.so; this module marshals arguments, builds
+the host-side `Histogram`/`ProtocolStats` result types and runs the ranking
+chain of `Search::sorted_evolving_configs` over device-computed stats.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import enum
+import itertools
+import math
+import os
+from dataclasses import dataclass
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import _lib
+from ._lib import check, lib, ptr, u32
+from .metrics import F64, Histogram, Stats
+from .planet import Planet, Region
+from .protocol import ClientPlacement, Protocol, ProtocolStats
+
+SLOT_KEYS = [(Protocol.Atlas, 1), (Protocol.FPaxos, 1), (Protocol.Atlas, 2), (Protocol.FPaxos, 2),
+             (Protocol.EPaxos, 0)]
+
+
+def max_f(n: int) -> int:
+    """search.rs:474-477"""
+    return min(n // 2, 2)
+
+
+class FTMetric(enum.Enum):
+    """search.rs:652-666"""
+    F1 = 1
+    F1F2 = 2
+
+    def fs(self, n: int) -> List[int]:
+        return list(range(1, min(n // 2, self.value) + 1))
+
+
+@dataclass
+class RankingParams:
+    """search.rs:617-649"""
+    min_mean_fpaxos_improv: float
+    min_mean_epaxos_improv: float
+    min_fairness_fpaxos_improv: float
+    min_mean_decrease: float
+    min_n: int
+    max_n: int
+    ft_metric: FTMetric
+
+    @classmethod
+    def new(cls, min_mean_fpaxos_improv: int, min_mean_epaxos_improv: int, min_fairness_fpaxos_improv: int,
+            min_mean_decrease: int, min_n: int, max_n: int, ft_metric: FTMetric) -> "RankingParams":
+        return cls(float(min_mean_fpaxos_improv), float(min_mean_epaxos_improv), float(min_fairness_fpaxos_improv),
+                   float(min_mean_decrease), min_n, max_n, ft_metric)
+
+
+# --------------------------------------------------------------- planet ---
+class DevicePlanet:
+    """A `Planet` resident on one GPU (bote_planet_create)."""
+
+    def __init__(self, planet: Planet, device: int = 0):
+        self.planet = planet
+        self.device = device
+        h = C.c_void_p()
+        check(lib().bote_planet_create(planet.lat, planet.R, device, C.byref(h)))
+        self.h = h
+
+    def __del__(self):
+        try:
+            if self.h:
+                lib().bote_planet_destroy(self.h)
+                self.h = None
+        except Exception:
+            pass
+
+
+# ----------------------------------------------------------------- eval ---
+@dataclass
+class EvalResult:
+    """Device outputs of `bote_eval` for a batch of configurations."""
+    n: int
+    nc: int
+    vals: Optional[np.ndarray]   # (ncfg, 5*nc + 5*n) uint32
+    leader: np.ndarray           # (ncfg,) position inside the config
+    s1: np.ndarray               # (ncfg, 10) uint64
+    s2: np.ndarray               # (ncfg, 10) uint64
+    mean: np.ndarray             # (ncfg, 10) f64 (bit-exact Histogram::mean)
+    cov: np.ndarray              # (ncfg, 10) f64
+    score: Optional[np.ndarray]
+    valid: Optional[np.ndarray]
+
+    def slot_values(self, i: int, slot: int) -> np.ndarray:
+        nc, n = self.nc, self.n
+        row = self.vals[i]
+        if slot < 5:
+            return row[slot * nc:(slot + 1) * nc]
+        return row[5 * nc + (slot - 5) * n:5 * nc + (slot - 4) * n]
+
+    def protocol_stats(self, i: int) -> ProtocolStats:
+        st = ProtocolStats.new()
+        for slot in range(10):
+            proto, f = SLOT_KEYS[slot % 5]
+            if proto is not Protocol.EPaxos and f > max_f(self.n):
+                continue
+            placement = ClientPlacement.Input if slot < 5 else ClientPlacement.Colocated
+            st.insert(proto, f, placement, Histogram.from_values(self.slot_values(i, slot).tolist()))
+        return st
+
+
+def eval_configs(dp: DevicePlanet, servers: Sequence[int], clients: Sequence[int], n: int,
+                 configs: Optional[np.ndarray] = None, rank_begin: int = 0, ncfg: Optional[int] = None,
+                 ranking: Optional[RankingParams] = None, values: bool = True) -> EvalResult:
+    """`Search::compute_stats` over a batch (explicit position lists or colex ranks)."""
+    srv, cli = u32(servers), u32(clients)
+    if configs is not None:
+        cfg = np.ascontiguousarray(np.asarray(configs, dtype=np.uint32).reshape(-1, n))
+        ncfg = cfg.shape[0]
+        cptr = ptr(cfg)
+    else:
+        cfg, cptr = None, None
+        if ncfg is None:
+            ncfg = _lib.binomial(len(srv), n) - rank_begin
+    nc = len(cli)
+    vals = np.zeros((ncfg, 5 * nc + 5 * n), np.uint32) if values else None
+    lead = np.zeros(ncfg, np.uint32)
+    s1 = np.zeros((ncfg, 10), np.uint64)
+    s2 = np.zeros((ncfg, 10), np.uint64)
+    mean = np.zeros((ncfg, 10), np.float64)
+    cov = np.zeros((ncfg, 10), np.float64)
+    score = np.zeros(ncfg, np.float64) if ranking else None
+    valid = np.zeros(ncfg, np.uint8) if ranking else None
+    rp = C.byref(_lib.ranking_params_c(ranking)) if ranking else None
+    check(lib().bote_eval(dp.h, srv, len(srv), cli, nc, n, cptr, rank_begin, ncfg, rp, ptr(vals), ptr(lead),
+                          ptr(s1), ptr(s2), ptr(mean), ptr(cov), ptr(score), ptr(valid)))
+    return EvalResult(n, nc, vals, lead, s1, s2, mean, cov, score, valid)
+
+
+# ----------------------------------------------------------------- Bote ---
+class Bote:
+    """lib.rs:16-186 — the analytic latency model over a device planet."""
+
+    def __init__(self, planet: Optional[Planet] = None, device: int = 0):
+        self.planet = planet if planet is not None else Planet.new()
+        self.dp = DevicePlanet(self.planet, device)
+
+    @classmethod
+    def new(cls, device: int = 0) -> "Bote":
+        return cls(Planet.new(), device)
+
+    @classmethod
+    def from_(cls, planet: Planet, device: int = 0) -> "Bote":
+        return cls(planet, device)
+
+    def _ids(self, regions) -> np.ndarray:
+        return self.planet.idxs(regions)
+
+    def quorum_latency(self, frm, regions: Sequence, quorum_size: int) -> int:
+        """lib.rs:155-163"""
+        out = np.zeros(1, np.uint64)
+        fr = u32([self.planet.idx(frm)])
+        regs = self._ids(regions)
+        check(lib().bote_quorum_latencies(self.dp.h, fr, 1, regs, len(regs), quorum_size, out))
+        return int(out[0])
+
+    def leaderless(self, servers: Sequence, clients: Sequence, quorum_size: int) -> List[Tuple[Region, int]]:
+        """lib.rs:38-59"""
+        s, c = self._ids(servers), self._ids(clients)
+        out = np.zeros(len(c), np.uint64)
+        check(lib().bote_leaderless(self.dp.h, s, len(s), c, len(c), quorum_size, out))
+        return [(Region(self.planet.names[i]), int(v)) for i, v in zip(c, out)]
+
+    def leader(self, leader, servers: Sequence, clients: Sequence, quorum_size: int) -> List[Tuple[Region, int]]:
+        """lib.rs:67-89"""
+        s, c = self._ids(servers), self._ids(clients)
+        out = np.zeros(len(c), np.uint64)
+        check(lib().bote_leader(self.dp.h, self.planet.idx(leader), s, len(s), c, len(c), quorum_size, out))
+        return [(Region(self.planet.names[i]), int(v)) for i, v in zip(c, out)]
+
+    def all_leaders_stats(self, servers: Sequence, clients: Sequence, quorum_size: int) -> List[Tuple[Region, Histogram]]:
+        """lib.rs:129-150"""
+        s, c = self._ids(servers), self._ids(clients)
+        out = np.zeros(len(s) * len(c), np.uint64)
+        check(lib().bote_all_leaders(self.dp.h, s, len(s), c, len(c), quorum_size, out))
+        out = out.reshape(len(s), len(c))
+        return [(Region(self.planet.names[l]), Histogram.from_values(out[i].tolist())) for i, l in enumerate(s)]
+
+    def best_leader(self, servers: Sequence, clients: Sequence, quorum_size: int,
+                    stats_sort_by: Stats) -> Tuple[Region, Histogram]:
+        """lib.rs:99-121"""
+        s, c = self._ids(servers), self._ids(clients)
+        pos = C.c_uint32()
+        lat = np.zeros(max(len(c), 1), np.uint64)
+        check(lib().bote_best_leader(self.dp.h, s, len(s), c, len(c), quorum_size, stats_sort_by.value,
+                                     C.byref(pos), ptr(lat)))
+        return Region(self.planet.names[s[pos.value]]), Histogram.from_values(lat[:len(c)].tolist())
+
+
+# --------------------------------------------------------------- Search ---
+class SearchInput(enum.Enum):
+    """search.rs:516-611"""
+    R13C13 = "R13C13"
+    R17C17 = "R17C17"
+    R20C20 = "R20C20"
+    R17CMaxN = "R17CMaxN"
+
+    def __str__(self):
+        return self.value
+
+    def get_inputs(self, max_n: int, planet: Planet) -> Tuple[Optional[List[Region]], List[List[Region]]]:
+        regions13 = [Region(x) for x in (
+            "asia-southeast1", "europe-west4", "southamerica-east1", "australia-southeast1", "europe-west2",
+            "asia-south1", "us-east1", "asia-northeast1", "europe-west1", "asia-east1", "us-west1",
+            "europe-west3", "us-central1")]
+        regions17 = [Region(x) for x in (
+            "asia-east1", "asia-northeast1", "asia-south1", "asia-southeast1", "australia-southeast1",
+            "europe-north1", "europe-west1", "europe-west2", "europe-west3", "europe-west4",
+            "northamerica-northeast1", "southamerica-east1", "us-central1", "us-east1", "us-east4", "us-west1",
+            "us-west2")]
+        all_regions = sorted(planet.regions())
+        if self is SearchInput.R13C13:
+            return regions13, [list(regions13)]
+        if self is SearchInput.R17C17:
+            return regions17, [list(regions17)]
+        if self is SearchInput.R20C20:
+            return all_regions, [list(all_regions)]
+        return None, [list(c) for c in itertools.combinations(regions17, max_n)]
+
+
+@dataclass
+class ConfigAndStats:
+    """(BTreeSet<Region>, ProtocolStats) of search.rs:24-25, with lazy stats."""
+    config: List[Region]          # name order (BTreeSet iteration order)
+    mask: int                     # bitmask of region ids
+    _search: "Search"
+    _key: Tuple[int, int, int]    # (client set index, n, config index)
+
+    @property
+    def stats(self) -> ProtocolStats:
+        return self._search._stats(*self._key)
+
+    def __iter__(self):
+        yield self.config
+        yield self.stats
+
+
+class Search:
+    """search.rs:41-512 — exhaustive search, computed on the GPU."""
+
+    BATCH = 1 << 18
+
+    def __init__(self, min_n: int, max_n: int, search_input: SearchInput, save_search: bool = False,
+                 lat_dir: Optional[str] = None, device: int = 0, planet: Optional[Planet] = None):
+        self.min_n, self.max_n, self.search_input = min_n, max_n, search_input
+        self.planet = planet if planet is not None else (Planet.from_dir(lat_dir) if lat_dir else Planet.new())
+        self.dp = DevicePlanet(self.planet, device)
+        filename = self.filename(min_n, max_n, search_input)
+        servers, all_clients = search_input.get_inputs(max_n, self.planet)
+        self.all_configs: List[Tuple[List[Region], Dict[int, dict]]] = []
+        loaded = self._load(filename) if os.path.exists(filename) else None
+        if loaded is not None:
+            self.all_configs = loaded
+        else:
+            for clients in all_clients:
+                srv = servers if servers is not None else clients
+                self.all_configs.append((clients, self._compute_configs(min_n, max_n, srv, clients)))
+            if save_search:
+                self._save(filename)
+        self._stats_cache: Dict[Tuple[int, int, int], ProtocolStats] = {}
+
+    @staticmethod
+    def filename(min_n: int, max_n: int, search_input: SearchInput) -> str:
+        """search.rs:479-485 (stored as .npz instead of bincode)."""
+        return f"{min_n}_{max_n}_{search_input}.npz"
+
+    # search.rs:234-260 — configs of each n in lexicographic order of positions.
+    def _compute_configs(self, min_n: int, max_n: int, servers: Sequence[Region], clients: Sequence[Region]):
+        srv_ids = self.planet.idxs(servers)
+        cli_ids = self.planet.idxs(clients)
+        out = {}
+        for n in range(min_n, max_n + 1, 2):
+            if n > len(srv_ids):
+                out[n] = dict(cfg=np.zeros((0, n), np.uint32), mean=np.zeros((0, 10)), s1=np.zeros((0, 10), np.uint64),
+                              srv=srv_ids, cli=cli_ids)
+                continue
+            cfg = np.array(list(itertools.combinations(range(len(srv_ids)), n)), dtype=np.uint32).reshape(-1, n)
+            means, s1s, covs = [], [], []
+            for b in range(0, len(cfg), self.BATCH):
+                r = eval_configs(self.dp, srv_ids, cli_ids, n, configs=cfg[b:b + self.BATCH], values=False)
+                means.append(r.mean)
+                s1s.append(r.s1)
+                covs.append(r.cov)
+            out[n] = dict(cfg=cfg, mean=np.concatenate(means), s1=np.concatenate(s1s), cov=np.concatenate(covs),
+                          srv=srv_ids, cli=cli_ids)
+        return out
+
+    def _save(self, filename: str):
+        arrs = {}
+        for ci, (clients, configs) in enumerate(self.all_configs):
+            arrs[f"c{ci}_clients"] = self.planet.idxs(clients)
+            for n, d in configs.items():
+                for k, v in d.items():
+                    arrs[f"c{ci}_n{n}_{k}"] = v
+        np.savez(filename, **arrs)
+
+    def _load(self, filename: str):
+        z = np.load(filename, allow_pickle=False)
+        out = []
+        ci = 0
+        while f"c{ci}_clients" in z:
+            clients = [Region(self.planet.names[i]) for i in z[f"c{ci}_clients"]]
+            configs = {}
+            for n in range(self.min_n, self.max_n + 1, 2):
+                d = {k: z[f"c{ci}_n{n}_{k}"] for k in ("cfg", "mean", "s1", "cov", "srv", "cli")
+                     if f"c{ci}_n{n}_{k}" in z}
+                configs[n] = d
+            out.append((clients, configs))
+            ci += 1
+        return out
+
+    def _stats(self, ci: int, n: int, i: int) -> ProtocolStats:
+        key = (ci, n, i)
+        if key not in self._stats_cache:
+            d = self.all_configs[ci][1][n]
+            r = eval_configs(self.dp, d["srv"], d["cli"], n, configs=d["cfg"][i:i + 1])
+            self._stats_cache[key] = r.protocol_stats(0)
+        return self._stats_cache[key]
+
+    def _config_set(self, ci: int, n: int, i: int) -> ConfigAndStats:
+        d = self.all_configs[ci][1][n]
+        ids = sorted(int(d["srv"][p]) for p in d["cfg"][i])
+        mask = 0
+        for r in ids:
+            mask |= 1 << r
+        return ConfigAndStats([Region(self.planet.names[r]) for r in ids], mask, self, (ci, n, i))
+
+    @staticmethod
+    def compute_stats(config: Sequence, all_clients: Sequence, bote: Bote) -> ProtocolStats:
+        """search.rs:262-319 for one configuration (config order = given order)."""
+        srv = bote.planet.idxs(config)
+        cli = bote.planet.idxs(all_clients)
+        n = len(srv)
+        r = eval_configs(bote.dp, srv, cli, n, configs=np.arange(n, dtype=np.uint32).reshape(1, n))
+        return r.protocol_stats(0)
+
+    # ------------------------------------------------------------ ranking ---
+    def _rank(self, configs: Dict[int, dict], p: RankingParams, ci: int):
+        """search.rs:329-354: valid configs and their scores, per n, in enumeration order.
+        Scores and validity come from the device (bote_eval with the ranking params)."""
+        ranked = {}
+        for n, d in configs.items():
+            if not (p.min_n <= n <= p.max_n):
+                continue
+            cfg = d["cfg"]
+            if len(cfg) == 0:
+                ranked[n] = []
+                continue
+            r = eval_configs(self.dp, d["srv"], d["cli"], n, configs=cfg, ranking=p, values=False)
+            idx = np.nonzero(r.valid)[0]
+            ranked[n] = [(float(r.score[i]), int(i)) for i in idx]
+        return ranked
+
+    def sorted_evolving_configs(self, p: RankingParams):
+        """search.rs:97-178: chains n = 3 -> 5 -> ... -> 13 of supersets, highest score first."""
+        assert p.min_n == 3 and p.max_n == 13
+        results: Dict[F64, list] = {}
+        for ci, (clients, configs) in enumerate(self.all_configs):
+            ranked = self._rank(configs, p, ci)
+            masks = {n: {i: self._config_set(ci, n, i) for _, i in lst} for n, lst in ranked.items()}
+            means = {n: configs[n]["mean"] for n in ranked}
+
+            def supers(n, prev_n, prev_i):
+                prev = masks[prev_n][prev_i]
+                fs = p.ft_metric.fs(n - 2)
+                out = []
+                for score, i in ranked[n]:
+                    cs = masks[n][i]
+                    if cs.mask & prev.mask != prev.mask:
+                        continue
+                    ok = True
+                    for f in fs:  # min_mean_decrease (search.rs:403-419)
+                        slot = 0 if f == 1 else 2
+                        if not (means[prev_n][prev_i, slot] - means[n][i, slot] >= p.min_mean_decrease):
+                            ok = False
+                            break
+                    if ok:
+                        out.append((score, i))
+                return out
+
+            for s3, i3 in ranked.get(3, []):
+                for s5, i5 in supers(5, 3, i3):
+                    for s7, i7 in supers(7, 5, i5):
+                        for s9, i9 in supers(9, 7, i7):
+                            for s11, i11 in supers(11, 9, i9):
+                                for s13, i13 in supers(13, 11, i11):
+                                    score = s3 + s5 + s7 + s9 + s11 + s13
+                                    chain = [masks[3][i3], masks[5][i5], masks[7][i7], masks[9][i9],
+                                             masks[11][i11], masks[13][i13]]
+                                    results.setdefault(F64(score), []).append((F64(score), chain, clients))
+        out = []
+        for key in sorted(results.keys(), reverse=True):
+            out.extend(results[key])
+        return out
+
+    @staticmethod
+    def stats_fmt(stats: ProtocolStats, n: int) -> str:
+        """search.rs:180-197"""
+        out = ""
+        for placement in ClientPlacement.all():
+            fmt = ""
+            for f in range(1, max_f(n) + 1):
+                fmt += f"{stats.fmt(Protocol.Atlas, f, placement)} {stats.fmt(Protocol.FPaxos, f, placement)} "
+            out += f"{fmt}{stats.fmt(Protocol.EPaxos, 0, placement)} "
+        return out
+
+
+# ---------------------------------------------------------------- sweep ---
+DEFAULT_OBJECTIVES = [(_lib.OBJ_SCORE, 0), (_lib.OBJ_MEAN, _lib.SLOT_AF1), (_lib.OBJ_MEAN, _lib.SLOT_FF1),
+                      (_lib.OBJ_COV, _lib.SLOT_AF1), (_lib.OBJ_MEAN, _lib.SLOT_E)]
+DEFAULT_RANKING = RankingParams.new(110, 35, 0, 15, 3, 13, FTMetric.F1F2)
+
+
+@dataclass
+class SweepResult:
+    tops: List[List[Tuple[int, int]]]  # per objective: (key, rank) ascending
+    valid: int
+    digest: int
+
+
+class Sweep:
+    """Streaming exhaustive search with a device top-K (bote_sweep_*)."""
+
+    def __init__(self, dp: DevicePlanet, servers: Sequence[int], clients: Sequence[int], n: int,
+                 objectives=DEFAULT_OBJECTIVES, K: int = 100, ranking: Optional[RankingParams] = DEFAULT_RANKING,
+                 digest: bool = False):
+        self.dp, self.n, self.K = dp, n, K
+        self.servers, self.clients = u32(servers), u32(clients)
+        self.objectives = list(objectives)
+        objs = (_lib.Objective * max(len(self.objectives), 1))(*[_lib.Objective(k, s) for k, s in self.objectives])
+        rp = C.byref(_lib.ranking_params_c(ranking)) if ranking is not None else None
+        h = C.c_void_p()
+        check(lib().bote_sweep_create(dp.h, self.servers, len(self.servers), self.clients, len(self.clients), n,
+                                      objs, len(self.objectives), K, rp, 1 if digest else 0, C.byref(h)))
+        self.h = h
+        self.total = _lib.binomial(len(self.servers), n)
+
+    def __del__(self):
+        try:
+            if self.h:
+                lib().bote_sweep_destroy(self.h)
+                self.h = None
+        except Exception:
+            pass
+
+    def launch(self, rank_begin: int = 0, rank_end: Optional[int] = None, stream: Optional[int] = None):
+        re = self.total if rank_end is None else rank_end
+        check(lib().bote_sweep_launch(self.h, rank_begin, re, C.c_void_p(stream) if stream else None))
+
+    def result(self, stream: Optional[int] = None) -> SweepResult:
+        no = len(self.objectives)
+        recs = (_lib.TopKRecord * (no * self.K))()
+        cnt = np.zeros(max(no, 1), np.uint32)
+        valid, digest = C.c_uint64(), C.c_uint64()
+        check(lib().bote_sweep_result(self.h, C.c_void_p(stream) if stream else None, recs, ptr(cnt),
+                                      C.byref(valid), C.byref(digest)))
+        tops = [[(recs[o * self.K + i].key, recs[o * self.K + i].rank) for i in range(cnt[o])] for o in range(no)]
+        return SweepResult(tops, valid.value, digest.value)
+
+    def result_bytes(self) -> int:
+        return int(lib().bote_sweep_result_bytes(self.h))
+
+    def result_device(self, dst_ptr: int, stream: Optional[int] = None):
+        check(lib().bote_sweep_result_device(self.h, C.c_void_p(dst_ptr), C.c_void_p(stream) if stream else None))
+
+    def merge_device(self, src_ptr: int, n_shards: int, dst_ptr: int, stream: Optional[int] = None):
+        check(lib().bote_merge_device(self.h, C.c_void_p(src_ptr), n_shards, C.c_void_p(dst_ptr),
+                                      C.c_void_p(stream) if stream else None))
+
+    def parse_block(self, blk: np.ndarray) -> SweepResult:
+        """Host view of a device result block (bote_sweep_result_device layout)."""
+        no, K = len(self.objectives), self.K
+        b = np.frombuffer(blk.tobytes(), dtype=np.uint64)
+        recs = b[:no * _lib.KP * 2].reshape(no, _lib.KP, 2)
+        tops = []
+        for o in range(no):
+            lst = []
+            for i in range(K):
+                k, r = int(recs[o, i, 0]), int(recs[o, i, 1])
+                if k == 0xFFFFFFFFFFFFFFFF and r == 0xFFFFFFFFFFFFFFFF:
+                    break
+                lst.append((k, r))
+            tops.append(lst)
+        return SweepResult(tops, int(b[no * _lib.KP * 2]), int(b[no * _lib.KP * 2 + 1]))
+
+    def kernel_ms(self) -> float:
+        v = C.c_float()
+        check(lib().bote_sweep_last_kernel_ms(self.h, C.byref(v)))
+        return v.value
+
+    def timing_reset(self):
+        check(lib().bote_sweep_timing_reset(self.h))
+
+    def timing(self) -> Tuple[float, int]:
+        """(total kernel ms, launches) since the last timing_reset."""
+        ms, n = C.c_float(), C.c_uint32()
+        check(lib().bote_sweep_timing(self.h, C.byref(ms), C.byref(n)))
+        return ms.value, n.value
+
+    def geometry(self) -> Tuple[int, int, int]:
+        g, b, l = C.c_uint32(), C.c_uint32(), C.c_uint32()
+        check(lib().bote_sweep_grid(self.h, C.byref(g), C.byref(b), C.byref(l)))
+        return g.value, b.value, l.value
+
+    def config_of(self, rank: int) -> List[int]:
+        pos = _lib.colex_unrank(rank, self.n, len(self.servers))
+        return [int(self.servers[p]) for p in pos]

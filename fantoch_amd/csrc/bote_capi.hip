@@ -1,0 +1,645 @@
+// bote_capi.hip — C ABI (include/bote_hip.h) over the gfx950 kernels.
+//
+// Host responsibilities only: argument validation (the reference panics, we
+// return BOTE_E_* codes), device buffers, launch geometry and the merge chain.
+// Every computation of latencies, quorums, leaders, histograms moments, scores
+// and top-K selection runs on the device (bote_kernels.hip).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/bote_hip.h"
+#include "bote_kernels.hpp"
+
+using bote::EvalArgs;
+using bote::Rec;
+using bote::SingleArgs;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                          \
+  do {                                                                                         \
+    hipError_t _e = (expr);                                                                    \
+    if (_e != hipSuccess) return fail(BOTE_E_DEVICE, std::string(#expr) + ": " + hipGetErrorString(_e)); \
+  } while (0)
+
+// RAII device buffer
+struct DBuf {
+  void* p = nullptr;
+  ~DBuf() {
+    if (p) (void)hipFree(p);
+  }
+  hipError_t alloc(size_t bytes) { return hipMalloc(&p, bytes ? bytes : 16); }
+  template <class T>
+  T* as() const { return (T*)p; }
+};
+
+uint64_t binom_u64(uint32_t m, uint32_t k) {
+  if (k > m) return 0;
+  k = std::min(k, m - k);
+  unsigned __int128 r = 1;
+  for (uint32_t i = 1; i <= k; ++i) {
+    r = r * (m - k + i) / i;
+    if (r > (unsigned __int128)UINT64_MAX) return 0;
+  }
+  return (uint64_t)r;
+}
+
+std::vector<uint64_t> binom_table(uint32_t ns, uint32_t n) {
+  std::vector<uint64_t> t((size_t)(ns + 1) * (n + 1), 0);
+  for (uint32_t m = 0; m <= ns; ++m)
+    for (uint32_t k = 0; k <= n; ++k) t[(size_t)m * (n + 1) + k] = binom_u64(m, k);
+  return t;
+}
+
+int check_regions(const uint32_t* ids, uint32_t n, uint32_t R, bool distinct, const char* what) {
+  if (n && !ids) return fail(BOTE_E_ARG, std::string(what) + " is null");
+  std::vector<uint8_t> seen(R, 0);
+  for (uint32_t i = 0; i < n; ++i) {
+    if (ids[i] >= R) return fail(BOTE_E_ARG, std::string(what) + ": region id out of range");
+    if (distinct && seen[ids[i]]++) return fail(BOTE_E_ARG, std::string(what) + ": duplicate region");
+  }
+  return BOTE_OK;
+}
+
+uint32_t distinct_count(const uint32_t* ids, uint32_t n, uint32_t R) {
+  std::vector<uint8_t> seen(R, 0);
+  uint32_t c = 0;
+  for (uint32_t i = 0; i < n; ++i)
+    if (!seen[ids[i]]++) ++c;
+  return c;
+}
+
+int device_cus(int dev) {
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return 256;
+  return prop.multiProcessorCount;
+}
+
+size_t device_max_lds(int dev) {
+  int v = 0;
+  if (hipDeviceGetAttribute(&v, hipDeviceAttributeMaxSharedMemoryPerBlock, dev) != hipSuccess || v <= 0)
+    return 160 * 1024;
+  return (size_t)std::max(v, 160 * 1024);
+}
+
+}  // namespace
+
+struct bote_planet {
+  int device;
+  uint32_t R;
+  std::vector<uint16_t> lat;
+  uint32_t* d_mat = nullptr;
+};
+
+struct bote_sweep {
+  const bote_planet* p = nullptr;
+  uint32_t n = 0, ns = 0, nc = 0, n_obj = 0, K = 0;
+  EvalArgs args{};
+  uint32_t grid = 0, bd = 0;
+  size_t shm = 0;
+  DBuf srv, cli, binom, top, tmp0, tmp1, result, counters;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  // per-launch kernel timing since the last bote_sweep_timing_reset
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> evpool;
+  size_t ev_used = 0;
+  bool launched = false;
+  uint64_t result_bytes() const { return (uint64_t)n_obj * bote::KP * 16 + 16; }
+};
+
+extern "C" {
+
+const char* bote_last_error(void) { return g_err.c_str(); }
+
+int bote_device_count(int* out) {
+  if (!out) return fail(BOTE_E_ARG, "out is null");
+  int c = 0;
+  hipError_t e = hipGetDeviceCount(&c);
+  if (e != hipSuccess) c = 0;
+  *out = c;
+  return BOTE_OK;
+}
+
+// ------------------------------------------------------------------ planet
+int bote_planet_create(const uint16_t* lat, uint32_t R, int device, bote_planet** out) {
+  if (!lat || !out) return fail(BOTE_E_ARG, "null argument");
+  if (R == 0 || R > BOTE_MAX_REGIONS) return fail(BOTE_E_RANGE, "R must be in [1, 128]");
+  for (size_t i = 0; i < (size_t)R * R; ++i)
+    if (lat[i] > BOTE_MAX_LATENCY) return fail(BOTE_E_RANGE, "latency above 16383");
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(BOTE_E_NODEV, "no HIP device");
+  if (device < 0 || device >= ndev) return fail(BOTE_E_ARG, "device out of range");
+  HIP_TRY(hipSetDevice(device));
+  auto* p = new bote_planet();
+  p->device = device;
+  p->R = R;
+  p->lat.assign(lat, lat + (size_t)R * R);
+  std::vector<uint32_t> m((size_t)R * R);
+  for (size_t i = 0; i < m.size(); ++i) m[i] = (uint32_t)lat[i] << bote::LAT_SHIFT;
+  if (hipMalloc(&p->d_mat, m.size() * 4) != hipSuccess) {
+    delete p;
+    return fail(BOTE_E_NOMEM, "hipMalloc planet");
+  }
+  if (hipMemcpy(p->d_mat, m.data(), m.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
+    (void)hipFree(p->d_mat);
+    delete p;
+    return fail(BOTE_E_DEVICE, "upload planet");
+  }
+  *out = p;
+  return BOTE_OK;
+}
+
+int bote_planet_destroy(bote_planet* p) {
+  if (!p) return BOTE_OK;
+  (void)hipSetDevice(p->device);
+  if (p->d_mat) (void)hipFree(p->d_mat);
+  delete p;
+  return BOTE_OK;
+}
+
+int bote_planet_regions(const bote_planet* p, uint32_t* out_R) {
+  if (!p || !out_R) return fail(BOTE_E_ARG, "null argument");
+  *out_R = p->R;
+  return BOTE_OK;
+}
+
+// ---------------------------------------------------------------- protocol
+int bote_quorum_size(int protocol, uint32_t n, uint32_t f) {
+  switch (protocol) {
+    case BOTE_FPAXOS: return (int)(f + 1);
+    case BOTE_EPAXOS: { uint32_t m = n / 2; return (int)(m + (m + 1) / 2); }
+    case BOTE_ATLAS: return (int)(n / 2 + f);
+    case BOTE_TEMPO: return (int)(n / 2 + f);
+    case BOTE_TEMPO_TINY: return (int)(2 * f);
+    default: return fail(BOTE_E_ARG, "unknown protocol");
+  }
+}
+
+uint32_t bote_max_f(uint32_t n) { return std::min(n / 2, 2u); }
+
+uint64_t bote_binomial(uint32_t ns, uint32_t n) { return binom_u64(ns, n); }
+
+int bote_colex_unrank(uint64_t rank, uint32_t n, uint32_t ns, uint32_t* out) {
+  if (!out || n > ns) return fail(BOTE_E_ARG, "bad unrank arguments");
+  uint64_t total = binom_u64(ns, n);
+  if (rank >= total) return fail(BOTE_E_ARG, "rank out of range");
+  uint64_t r = rank;
+  uint32_t hi = ns;
+  for (int j = (int)n - 1; j >= 0; --j) {
+    uint32_t k = j + 1, x = hi - 1;
+    while (x > (uint32_t)j && binom_u64(x, k) > r) --x;
+    out[j] = x;
+    r -= binom_u64(x, k);
+    hi = x;
+  }
+  return BOTE_OK;
+}
+
+// --------------------------------------------------- single configuration
+static int run_single(const bote_planet* p, const uint32_t* servers, uint32_t ns, const uint32_t* clients, uint32_t nc,
+                      const uint32_t* froms, uint32_t nf, uint32_t q, uint32_t leader, int mode, uint64_t* out,
+                      size_t nout) {
+  if (!p || !out) return fail(BOTE_E_ARG, "null argument");
+  int rc;
+  if ((rc = check_regions(servers, ns, p->R, false, "servers"))) return rc;
+  if ((rc = check_regions(clients, nc, p->R, false, "clients"))) return rc;
+  if ((rc = check_regions(froms, nf, p->R, false, "froms"))) return rc;
+  if (mode == 2 && leader >= p->R) return fail(BOTE_E_ARG, "leader out of range");
+  if (q == 0) return fail(BOTE_E_ARG, "quorum size 0");
+  if (q > distinct_count(servers, ns, p->R)) return fail(BOTE_E_QUORUM_GT_N, "quorum larger than the server set");
+  HIP_TRY(hipSetDevice(p->device));
+  DBuf ds, dc, df, dout;
+  HIP_TRY(ds.alloc(ns * 4));
+  HIP_TRY(dc.alloc(nc * 4));
+  HIP_TRY(df.alloc(nf * 4));
+  HIP_TRY(dout.alloc(nout * 8));
+  if (ns) HIP_TRY(hipMemcpy(ds.p, servers, ns * 4, hipMemcpyHostToDevice));
+  if (nc) HIP_TRY(hipMemcpy(dc.p, clients, nc * 4, hipMemcpyHostToDevice));
+  if (nf) HIP_TRY(hipMemcpy(df.p, froms, nf * 4, hipMemcpyHostToDevice));
+  SingleArgs a{};
+  a.mat = p->d_mat;
+  a.R = p->R;
+  a.servers = ds.as<uint32_t>();
+  a.ns = ns;
+  a.clients = dc.as<uint32_t>();
+  a.nc = nc;
+  a.froms = df.as<uint32_t>();
+  a.nf = nf;
+  a.q = q;
+  a.leader = leader;
+  a.out = dout.as<uint64_t>();
+  HIP_TRY(bote::launch_single(a, mode, nullptr));
+  HIP_TRY(hipDeviceSynchronize());
+  if (nout) HIP_TRY(hipMemcpy(out, dout.p, nout * 8, hipMemcpyDeviceToHost));
+  return BOTE_OK;
+}
+
+int bote_quorum_latencies(const bote_planet* p, const uint32_t* froms, uint32_t nf, const uint32_t* regions,
+                          uint32_t nr, uint32_t q, uint64_t* out) {
+  return run_single(p, regions, nr, nullptr, 0, froms, nf, q, 0, 0, out, nf);
+}
+
+int bote_leaderless(const bote_planet* p, const uint32_t* servers, uint32_t ns, const uint32_t* clients, uint32_t nc,
+                    uint32_t q, uint64_t* out) {
+  return run_single(p, servers, ns, clients, nc, nullptr, 0, q, 0, 1, out, nc);
+}
+
+int bote_leader(const bote_planet* p, uint32_t leader, const uint32_t* servers, uint32_t ns, const uint32_t* clients,
+                uint32_t nc, uint32_t q, uint64_t* out) {
+  return run_single(p, servers, ns, clients, nc, nullptr, 0, q, leader, 2, out, nc);
+}
+
+int bote_all_leaders(const bote_planet* p, const uint32_t* servers, uint32_t ns, const uint32_t* clients, uint32_t nc,
+                     uint32_t q, uint64_t* out) {
+  return run_single(p, servers, ns, clients, nc, nullptr, 0, q, 0, 3, out, (size_t)ns * nc);
+}
+
+int bote_best_leader(const bote_planet* p, const uint32_t* servers, uint32_t ns, const uint32_t* clients, uint32_t nc,
+                     uint32_t q, int stat, uint32_t* out_pos, uint64_t* out_lat) {
+  if (!p || !out_pos) return fail(BOTE_E_ARG, "null argument");
+  if (ns == 0) return fail(BOTE_E_ARG, "the best leader should exist (empty server list)");
+  if (stat < 0 || stat > 2) return fail(BOTE_E_ARG, "unknown stat");
+  int rc;
+  if ((rc = check_regions(servers, ns, p->R, false, "servers"))) return rc;
+  if ((rc = check_regions(clients, nc, p->R, false, "clients"))) return rc;
+  if (q == 0) return fail(BOTE_E_ARG, "quorum size 0");
+  if (q > distinct_count(servers, ns, p->R)) return fail(BOTE_E_QUORUM_GT_N, "quorum larger than the server set");
+  HIP_TRY(hipSetDevice(p->device));
+  DBuf ds, dc, dv, dstat, dpos;
+  HIP_TRY(ds.alloc(ns * 4));
+  HIP_TRY(dc.alloc(nc * 4));
+  HIP_TRY(dv.alloc((size_t)ns * nc * 8));
+  HIP_TRY(dstat.alloc(ns * 8));
+  HIP_TRY(dpos.alloc(4));
+  HIP_TRY(hipMemcpy(ds.p, servers, ns * 4, hipMemcpyHostToDevice));
+  if (nc) HIP_TRY(hipMemcpy(dc.p, clients, nc * 4, hipMemcpyHostToDevice));
+  SingleArgs a{};
+  a.mat = p->d_mat;
+  a.R = p->R;
+  a.servers = ds.as<uint32_t>();
+  a.ns = ns;
+  a.clients = dc.as<uint32_t>();
+  a.nc = nc;
+  a.q = q;
+  a.stat = stat;
+  a.out = dv.as<uint64_t>();
+  a.out_pos = dpos.as<uint32_t>();
+  HIP_TRY(bote::launch_single(a, 3, nullptr));
+  HIP_TRY(bote::launch_best_leader(a, dv.as<uint64_t>(), dstat.as<double>(), nullptr));
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpy(out_pos, dpos.p, 4, hipMemcpyDeviceToHost));
+  if (out_lat && nc)
+    HIP_TRY(hipMemcpy(out_lat, dv.as<uint64_t>() + (size_t)(*out_pos) * nc, nc * 8, hipMemcpyDeviceToHost));
+  return BOTE_OK;
+}
+
+// ------------------------------------------------------- common validation
+static int check_search_args(const bote_planet* p, const uint32_t* servers, uint32_t ns, const uint32_t* clients,
+                             uint32_t nc, uint32_t n) {
+  if (!p) return fail(BOTE_E_ARG, "planet is null");
+  if (n < 2) return fail(BOTE_E_QUORUM_GT_N, "config size must be >= 2 (FPaxos q = 2)");
+  if (n > BOTE_MAX_N) return fail(BOTE_E_RANGE, "config size above 16");
+  if (n > ns) return fail(BOTE_E_ARG, "config size larger than the server list");
+  if (nc > BOTE_MAX_CLIENTS) return fail(BOTE_E_RANGE, "more than 4096 clients");
+  int rc;
+  if ((rc = check_regions(servers, ns, p->R, true, "servers"))) return rc;
+  if ((rc = check_regions(clients, nc, p->R, false, "clients"))) return rc;
+  return BOTE_OK;
+}
+
+static void fill_rank_params(EvalArgs& a, const bote_ranking_params* rp) {
+  a.want_score = rp ? 1 : 0;
+  if (rp) {
+    a.p_fmean = rp->min_mean_fpaxos_improv;
+    a.p_emean = rp->min_mean_epaxos_improv;
+    a.p_fair = rp->min_fairness_fpaxos_improv;
+    a.ft_metric = rp->ft_metric;
+  }
+}
+
+// ------------------------------------------------------------------- eval
+int bote_eval(const bote_planet* p, const uint32_t* servers, uint32_t ns, const uint32_t* clients, uint32_t nc,
+              uint32_t n, const uint32_t* configs, uint64_t rank_begin, uint64_t ncfg, const bote_ranking_params* rp,
+              uint32_t* out_vals, uint32_t* out_leader, uint64_t* out_sum, uint64_t* out_sumsq, double* out_mean,
+              double* out_cov, double* out_score, uint8_t* out_valid) {
+  int rc;
+  if ((rc = check_search_args(p, servers, ns, clients, nc, n))) return rc;
+  if (rp && rp->ft_metric != BOTE_FT_F1 && rp->ft_metric != BOTE_FT_F1F2) return fail(BOTE_E_ARG, "bad ft_metric");
+  if (ncfg == 0) return BOTE_OK;
+  if (configs) {
+    for (uint64_t i = 0; i < ncfg; ++i) {
+      uint32_t seen[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      for (uint32_t j = 0; j < n; ++j) {
+        uint32_t x = configs[i * n + j];
+        if (x >= ns) return fail(BOTE_E_ARG, "config position out of range");
+        if (seen[x >> 5] & (1u << (x & 31))) return fail(BOTE_E_ARG, "duplicate position in config");
+        seen[x >> 5] |= 1u << (x & 31);
+      }
+    }
+  } else {
+    uint64_t total = binom_u64(ns, n);
+    if (rank_begin > total || ncfg > total - rank_begin) return fail(BOTE_E_ARG, "rank range out of bounds");
+  }
+  HIP_TRY(hipSetDevice(p->device));
+  const size_t stride = 5ull * nc + 5ull * n;
+  DBuf ds, dc, dcfg, dbin, dvals, dlead, ds1, ds2, dmean, dcov, dscore, dvalid;
+  HIP_TRY(ds.alloc(ns * 4));
+  HIP_TRY(dc.alloc(nc * 4));
+  HIP_TRY(hipMemcpy(ds.p, servers, ns * 4, hipMemcpyHostToDevice));
+  if (nc) HIP_TRY(hipMemcpy(dc.p, clients, nc * 4, hipMemcpyHostToDevice));
+  EvalArgs a{};
+  a.mat = p->d_mat;
+  a.R = p->R;
+  a.srv = ds.as<uint32_t>();
+  a.ns = ns;
+  a.cli = dc.as<uint32_t>();
+  a.nc = nc;
+  a.srv_sorted = std::is_sorted(servers, servers + ns) ? 1 : 0;
+  if (configs) {
+    HIP_TRY(dcfg.alloc(ncfg * n * 4));
+    HIP_TRY(hipMemcpy(dcfg.p, configs, ncfg * n * 4, hipMemcpyHostToDevice));
+    a.cfgs = dcfg.as<uint32_t>();
+    a.rb = 0;
+    a.re = ncfg;
+  } else {
+    auto t = binom_table(ns, n);
+    HIP_TRY(dbin.alloc(t.size() * 8));
+    HIP_TRY(hipMemcpy(dbin.p, t.data(), t.size() * 8, hipMemcpyHostToDevice));
+    a.binom = dbin.as<uint64_t>();
+    a.rb = rank_begin;
+    a.re = rank_begin + ncfg;
+  }
+  a.runlen = 1;
+  fill_rank_params(a, rp);
+  if (out_vals) { HIP_TRY(dvals.alloc(ncfg * stride * 4)); a.out_vals = dvals.as<uint32_t>(); }
+  if (out_leader) { HIP_TRY(dlead.alloc(ncfg * 4)); a.out_leader = dlead.as<uint32_t>(); }
+  if (out_sum) { HIP_TRY(ds1.alloc(ncfg * bote::NSLOT * 8)); a.out_s1 = ds1.as<uint64_t>(); }
+  if (out_sumsq) { HIP_TRY(ds2.alloc(ncfg * bote::NSLOT * 8)); a.out_s2 = ds2.as<uint64_t>(); }
+  if (out_mean) { HIP_TRY(dmean.alloc(ncfg * bote::NSLOT * 8)); a.out_mean = dmean.as<double>(); }
+  if (out_cov) { HIP_TRY(dcov.alloc(ncfg * bote::NSLOT * 8)); a.out_cov = dcov.as<double>(); }
+  if (out_score && rp) { HIP_TRY(dscore.alloc(ncfg * 8)); a.out_score = dscore.as<double>(); }
+  if (out_valid && rp) { HIP_TRY(dvalid.alloc(ncfg)); a.out_valid = dvalid.as<uint8_t>(); }
+
+  const uint32_t bd = 256;
+  size_t shm = bote::eval_smem_bytes(a, n, bd, false);
+  if (shm > device_max_lds(p->device)) return fail(BOTE_E_RANGE, "planet/client set too large for LDS");
+  int nb = bote::eval_occupancy(n, true, bd, shm);
+  uint64_t want = (ncfg + bd - 1) / bd;
+  uint32_t grid = (uint32_t)std::min<uint64_t>(want, (uint64_t)device_cus(p->device) * nb);
+  HIP_TRY(bote::launch_eval(a, n, true, grid, bd, shm, nullptr));
+  HIP_TRY(hipDeviceSynchronize());
+  if (out_vals) HIP_TRY(hipMemcpy(out_vals, dvals.p, ncfg * stride * 4, hipMemcpyDeviceToHost));
+  if (out_leader) HIP_TRY(hipMemcpy(out_leader, dlead.p, ncfg * 4, hipMemcpyDeviceToHost));
+  if (out_sum) HIP_TRY(hipMemcpy(out_sum, ds1.p, ncfg * bote::NSLOT * 8, hipMemcpyDeviceToHost));
+  if (out_sumsq) HIP_TRY(hipMemcpy(out_sumsq, ds2.p, ncfg * bote::NSLOT * 8, hipMemcpyDeviceToHost));
+  if (out_mean) HIP_TRY(hipMemcpy(out_mean, dmean.p, ncfg * bote::NSLOT * 8, hipMemcpyDeviceToHost));
+  if (out_cov) HIP_TRY(hipMemcpy(out_cov, dcov.p, ncfg * bote::NSLOT * 8, hipMemcpyDeviceToHost));
+  if (out_score && rp) HIP_TRY(hipMemcpy(out_score, dscore.p, ncfg * 8, hipMemcpyDeviceToHost));
+  if (out_valid && rp) HIP_TRY(hipMemcpy(out_valid, dvalid.p, ncfg, hipMemcpyDeviceToHost));
+  return BOTE_OK;
+}
+
+// ------------------------------------------------------------------ sweep
+int bote_sweep_create(const bote_planet* p, const uint32_t* servers, uint32_t ns, const uint32_t* clients,
+                      uint32_t nc, uint32_t n, const bote_objective* objs, uint32_t n_obj, uint32_t K,
+                      const bote_ranking_params* rp, int digest, bote_sweep** out) {
+  int rc;
+  if (!out) return fail(BOTE_E_ARG, "out is null");
+  if ((rc = check_search_args(p, servers, ns, clients, nc, n))) return rc;
+  if (n_obj > BOTE_MAX_OBJECTIVES) return fail(BOTE_E_RANGE, "more than 8 objectives");
+  if (n_obj && !objs) return fail(BOTE_E_ARG, "objectives null");
+  if (K == 0 || K > BOTE_MAX_K) return fail(BOTE_E_RANGE, "K must be in [1, 128]");
+  bool has_score = false;
+  for (uint32_t o = 0; o < n_obj; ++o) {
+    if (objs[o].kind > BOTE_OBJ_COV) return fail(BOTE_E_ARG, "unknown objective kind");
+    if (objs[o].kind == BOTE_OBJ_SCORE) {
+      has_score = true;
+      continue;
+    }
+    if (objs[o].slot >= BOTE_NSLOTS) return fail(BOTE_E_ARG, "slot out of range");
+    uint32_t b = objs[o].slot % 5;
+    if ((b == BOTE_SLOT_AF2 || b == BOTE_SLOT_FF2) && bote_max_f(n) < 2)
+      return fail(BOTE_E_ARG, "slot does not exist for this n (max_f < 2)");
+  }
+  if (has_score && !rp) return fail(BOTE_E_ARG, "SCORE objective needs ranking params");
+  if (rp && rp->ft_metric != BOTE_FT_F1 && rp->ft_metric != BOTE_FT_F1F2) return fail(BOTE_E_ARG, "bad ft_metric");
+  HIP_TRY(hipSetDevice(p->device));
+  auto* s = new bote_sweep();
+  auto cleanup = [&](int code) {
+    bote_sweep_destroy(s);
+    return code;
+  };
+  s->p = p;
+  s->n = n;
+  s->ns = ns;
+  s->nc = nc;
+  s->n_obj = n_obj;
+  s->K = K;
+  EvalArgs& a = s->args;
+  a = EvalArgs{};
+  auto t = binom_table(ns, n);
+  if (s->srv.alloc(ns * 4) != hipSuccess || s->cli.alloc(nc * 4) != hipSuccess ||
+      s->binom.alloc(t.size() * 8) != hipSuccess || s->counters.alloc(16) != hipSuccess)
+    return cleanup(fail(BOTE_E_NOMEM, "hipMalloc sweep lists"));
+  if (hipMemcpy(s->srv.p, servers, ns * 4, hipMemcpyHostToDevice) != hipSuccess ||
+      (nc && hipMemcpy(s->cli.p, clients, nc * 4, hipMemcpyHostToDevice) != hipSuccess) ||
+      hipMemcpy(s->binom.p, t.data(), t.size() * 8, hipMemcpyHostToDevice) != hipSuccess)
+    return cleanup(fail(BOTE_E_DEVICE, "upload sweep lists"));
+  a.mat = p->d_mat;
+  a.R = p->R;
+  a.srv = s->srv.as<uint32_t>();
+  a.ns = ns;
+  a.cli = s->cli.as<uint32_t>();
+  a.nc = nc;
+  a.srv_sorted = std::is_sorted(servers, servers + ns) ? 1 : 0;
+  a.binom = s->binom.as<uint64_t>();
+  fill_rank_params(a, has_score ? rp : nullptr);
+  a.n_obj = (int)n_obj;
+  for (uint32_t o = 0; o < n_obj; ++o) {
+    a.obj_kind[o] = objs[o].kind;
+    a.obj_slot[o] = objs[o].slot;
+  }
+  a.K = K;
+  a.want_digest = digest ? 1 : 0;
+  a.out_counters = s->counters.as<unsigned long long>();
+
+  s->bd = 256;
+  a.out_top = (Rec*)1;  // sizing with top-K structures
+  s->shm = bote::eval_smem_bytes(a, n, s->bd, true);
+  a.out_top = nullptr;
+  if (s->shm > device_max_lds(p->device)) return cleanup(fail(BOTE_E_RANGE, "planet/client set too large for LDS"));
+  int nb = bote::eval_occupancy(n, false, s->bd, s->shm);
+  s->grid = (uint32_t)(device_cus(p->device) * nb);
+  size_t top_bytes = (size_t)s->grid * std::max<uint32_t>(n_obj, 1) * bote::KP * 16;
+  size_t tmp_bytes = (size_t)((s->grid + 7) / 8) * std::max<uint32_t>(n_obj, 1) * bote::KP * 16;
+  if (s->top.alloc(top_bytes) != hipSuccess || s->tmp0.alloc(tmp_bytes) != hipSuccess ||
+      s->tmp1.alloc(tmp_bytes) != hipSuccess || s->result.alloc(s->result_bytes()) != hipSuccess)
+    return cleanup(fail(BOTE_E_NOMEM, "hipMalloc sweep workspace"));
+  a.out_top = n_obj ? s->top.as<Rec>() : nullptr;
+  if (hipEventCreate(&s->ev0) != hipSuccess || hipEventCreate(&s->ev1) != hipSuccess)
+    return cleanup(fail(BOTE_E_DEVICE, "hipEventCreate"));
+  *out = s;
+  return BOTE_OK;
+}
+
+int bote_sweep_launch(bote_sweep* s, uint64_t rank_begin, uint64_t rank_end, void* hip_stream) {
+  if (!s) return fail(BOTE_E_ARG, "sweep is null");
+  uint64_t total = binom_u64(s->ns, s->n);
+  if (rank_begin > rank_end || rank_end > total) return fail(BOTE_E_ARG, "rank range out of bounds");
+  HIP_TRY(hipSetDevice(s->p->device));
+  hipStream_t st = (hipStream_t)hip_stream;
+  EvalArgs a = s->args;
+  a.rb = rank_begin;
+  a.re = rank_end;
+  const uint64_t count = rank_end - rank_begin;
+  const uint64_t G = (uint64_t)s->grid * s->bd;
+  a.runlen = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(32, count / (G * 8)));
+  HIP_TRY(hipMemsetAsync(s->counters.p, 0, 16, st));
+  if (s->ev_used == s->evpool.size()) {
+    hipEvent_t e0, e1;
+    HIP_TRY(hipEventCreate(&e0));
+    HIP_TRY(hipEventCreate(&e1));
+    s->evpool.emplace_back(e0, e1);
+  }
+  auto& tp = s->evpool[s->ev_used++];
+  HIP_TRY(hipEventRecord(s->ev0, st));
+  HIP_TRY(hipEventRecord(tp.first, st));
+  HIP_TRY(bote::launch_eval(a, s->n, false, s->grid, s->bd, s->shm, st));
+  HIP_TRY(hipEventRecord(tp.second, st));
+  HIP_TRY(hipEventRecord(s->ev1, st));
+  // merge the per-block lists down to one: [o][KP] at the head of `result`
+  const uint64_t lstride = (uint64_t)s->n_obj * bote::KP;
+  Rec* rec_out = s->result.as<Rec>();
+  if (s->n_obj) {
+    uint32_t lists = s->grid;
+    const Rec* src = s->top.as<Rec>();
+    Rec* bufs[2] = {s->tmp0.as<Rec>(), s->tmp1.as<Rec>()};
+    int b = 0;
+    while (lists > bote::G_MERGE_LISTS) {
+      HIP_TRY(bote::launch_merge(src, lists, lstride, bufs[b], lstride, s->n_obj, st));
+      src = bufs[b];
+      b ^= 1;
+      lists = (lists + bote::G_MERGE_LISTS - 1) / bote::G_MERGE_LISTS;
+    }
+    HIP_TRY(bote::launch_merge(src, lists, lstride, rec_out, lstride, s->n_obj, st));
+  }
+  HIP_TRY(hipMemcpyAsync((char*)s->result.p + lstride * 16, s->counters.p, 16, hipMemcpyDeviceToDevice, st));
+  s->launched = true;
+  return BOTE_OK;
+}
+
+uint64_t bote_sweep_result_bytes(const bote_sweep* s) { return s ? s->result_bytes() : 0; }
+
+int bote_sweep_result_device(bote_sweep* s, void* dst, void* hip_stream) {
+  if (!s || !dst) return fail(BOTE_E_ARG, "null argument");
+  if (!s->launched) return fail(BOTE_E_ARG, "sweep not launched");
+  HIP_TRY(hipSetDevice(s->p->device));
+  HIP_TRY(hipMemcpyAsync(dst, s->result.p, s->result_bytes(), hipMemcpyDeviceToDevice, (hipStream_t)hip_stream));
+  return BOTE_OK;
+}
+
+static void unpack_result(const bote_sweep* s, const std::vector<uint8_t>& blk, bote_topk_record* out,
+                          uint32_t* out_count, uint64_t* out_valid, uint64_t* out_digest) {
+  const Rec* r = (const Rec*)blk.data();
+  for (uint32_t o = 0; o < s->n_obj; ++o) {
+    uint32_t c = 0;
+    for (uint32_t i = 0; i < s->K; ++i) {
+      Rec x = r[(size_t)o * bote::KP + i];
+      if (x.key == ~0ull && x.rank == ~0ull) break;
+      if (out) out[(size_t)o * s->K + i] = bote_topk_record{x.key, x.rank};
+      ++c;
+    }
+    for (uint32_t i = c; out && i < s->K; ++i) out[(size_t)o * s->K + i] = bote_topk_record{~0ull, ~0ull};
+    if (out_count) out_count[o] = c;
+  }
+  const uint64_t* cnt = (const uint64_t*)(blk.data() + (size_t)s->n_obj * bote::KP * 16);
+  if (out_valid) *out_valid = cnt[0];
+  if (out_digest) *out_digest = cnt[1];
+}
+
+int bote_sweep_result(bote_sweep* s, void* hip_stream, bote_topk_record* out, uint32_t* out_count,
+                      uint64_t* out_valid, uint64_t* out_digest) {
+  if (!s) return fail(BOTE_E_ARG, "sweep is null");
+  if (!s->launched) return fail(BOTE_E_ARG, "sweep not launched");
+  HIP_TRY(hipSetDevice(s->p->device));
+  std::vector<uint8_t> blk(s->result_bytes());
+  HIP_TRY(hipMemcpyAsync(blk.data(), s->result.p, blk.size(), hipMemcpyDeviceToHost, (hipStream_t)hip_stream));
+  HIP_TRY(hipStreamSynchronize((hipStream_t)hip_stream));
+  unpack_result(s, blk, out, out_count, out_valid, out_digest);
+  return BOTE_OK;
+}
+
+int bote_merge_device(const bote_sweep* s, const void* src, uint32_t n_shards, void* dst, void* hip_stream) {
+  if (!s || !src || !dst || n_shards == 0) return fail(BOTE_E_ARG, "bad merge arguments");
+  if (n_shards > bote::G_MERGE_LISTS) return fail(BOTE_E_RANGE, "at most 8 shards per merge call");
+  HIP_TRY(hipSetDevice(s->p->device));
+  hipStream_t st = (hipStream_t)hip_stream;
+  const uint64_t bstride = s->result_bytes() / 16;  // records per block
+  const uint64_t lstride = (uint64_t)s->n_obj * bote::KP;
+  if (s->n_obj) HIP_TRY(bote::launch_merge((const Rec*)src, n_shards, bstride, (Rec*)dst, lstride, s->n_obj, st));
+  HIP_TRY(bote::launch_sum_counters((const uint64_t*)src, n_shards, bstride * 2, lstride * 2,
+                                    (uint64_t*)dst + lstride * 2, st));
+  return BOTE_OK;
+}
+
+int bote_sweep_last_kernel_ms(bote_sweep* s, float* out_ms) {
+  if (!s || !out_ms) return fail(BOTE_E_ARG, "null argument");
+  if (!s->launched) return fail(BOTE_E_ARG, "sweep not launched");
+  HIP_TRY(hipEventSynchronize(s->ev1));
+  HIP_TRY(hipEventElapsedTime(out_ms, s->ev0, s->ev1));
+  return BOTE_OK;
+}
+
+int bote_sweep_timing_reset(bote_sweep* s) {
+  if (!s) return fail(BOTE_E_ARG, "sweep is null");
+  s->ev_used = 0;
+  return BOTE_OK;
+}
+
+int bote_sweep_timing(bote_sweep* s, float* out_total_ms, uint32_t* out_launches) {
+  if (!s || !out_total_ms || !out_launches) return fail(BOTE_E_ARG, "null argument");
+  HIP_TRY(hipSetDevice(s->p->device));
+  float tot = 0.f;
+  for (size_t i = 0; i < s->ev_used; ++i) {
+    float ms = 0.f;
+    HIP_TRY(hipEventSynchronize(s->evpool[i].second));
+    HIP_TRY(hipEventElapsedTime(&ms, s->evpool[i].first, s->evpool[i].second));
+    tot += ms;
+  }
+  *out_total_ms = tot;
+  *out_launches = (uint32_t)s->ev_used;
+  return BOTE_OK;
+}
+
+int bote_sweep_grid(const bote_sweep* s, uint32_t* out_grid, uint32_t* out_block, uint32_t* out_lds_bytes) {
+  if (!s) return fail(BOTE_E_ARG, "sweep is null");
+  if (out_grid) *out_grid = s->grid;
+  if (out_block) *out_block = s->bd;
+  if (out_lds_bytes) *out_lds_bytes = (uint32_t)s->shm;
+  return BOTE_OK;
+}
+
+int bote_sweep_destroy(bote_sweep* s) {
+  if (!s) return BOTE_OK;
+  (void)hipSetDevice(s->p ? s->p->device : 0);
+  for (auto& e : s->evpool) {
+    (void)hipEventDestroy(e.first);
+    (void)hipEventDestroy(e.second);
+  }
+  if (s->ev0) (void)hipEventDestroy(s->ev0);
+  if (s->ev1) (void)hipEventDestroy(s->ev1);
+  delete s;
+  return BOTE_OK;
+}
+
+}  // extern "C"

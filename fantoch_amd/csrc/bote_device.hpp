@@ -1,0 +1,248 @@
+// bote_device.hpp — device-side building blocks for the gfx950 configuration
+// search.  Integer min/select work on VALU; no MFMA (DESIGN.md "Roofline").
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace bote {
+
+constexpr int MAXN = 16;
+constexpr int KP = 128;      // top-K list capacity per objective (K <= KP)
+constexpr int MAXOBJ = 8;
+constexpr uint32_t LAT_SHIFT = 4;  // LDS matrix holds latency << 4; low 4 bits = member index
+
+// ------------------------------------------------------- compile-time config
+// Quorum sizes for a config of size N (fantoch_bote/src/protocol.rs:20-35,
+// search.rs:474-477).  Leaderless keys af1/af2/e need the q-th closest server
+// of the client's nearest server; those q's (deduplicated) are "LQ".
+template <int N>
+struct QCfg {
+  static constexpr int maxf = (N / 2 < 2) ? N / 2 : 2;
+  static constexpr int m = N / 2;
+  static constexpr int qa1 = m + 1;
+  static constexpr int qa2 = m + 2;
+  static constexpr int qe = m + (m + 1) / 2;
+  static constexpr int qf1 = 2;
+  static constexpr int qf2 = 3;
+  // leaderless distinct q list
+  static constexpr int lq0 = qa1;
+  static constexpr bool a2_new = (maxf >= 2) && (qa2 != qa1);
+  static constexpr int lq1 = a2_new ? qa2 : qe;
+  static constexpr bool e_new = (qe != qa1) && !(maxf >= 2 && qe == qa2);
+  static constexpr int NL = 1 + (a2_new ? 1 : 0) + (e_new ? 1 : 0);
+  static constexpr int lq2 = qe;
+  static constexpr int idx_a1 = 0;
+  static constexpr int idx_a2 = a2_new ? 1 : 0;
+  static constexpr int idx_e = (qe == qa1) ? 0 : ((maxf >= 2 && qe == qa2) ? 1 : (a2_new ? 2 : 1));
+  __host__ __device__ static constexpr int lq(int i) { return i == 0 ? lq0 : (i == 1 ? (a2_new ? qa2 : qe) : qe); }
+};
+
+// ----------------------------------------------------------- small helpers
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+__device__ __forceinline__ uint64_t orderable_f64(double x) {
+  if (x != x) x = __longlong_as_double(0x7FF8000000000000ll);
+  uint64_t b = (uint64_t)__double_as_longlong(x);
+  return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
+}
+
+// F64 total order (fantoch/src/metrics/float.rs:62-79): NaN greatest.
+__device__ __forceinline__ int f64_cmp(double a, double b) {
+  if (a < b) return -1;
+  if (a > b) return 1;
+  if (a == b) return 0;
+  bool an = a != a, bn = b != b;
+  if (an && bn) return 0;
+  return an ? 1 : -1;
+}
+
+// Batcher odd-even merge sort network over a[0..P), P a power of two,
+// fully unrolled (all indices are compile-time constants).
+template <int P, typename T>
+__device__ __forceinline__ void sort_network(T* a) {
+#pragma unroll
+  for (int p = 1; p < P; p <<= 1) {
+#pragma unroll
+    for (int k = p; k >= 1; k >>= 1) {
+#pragma unroll
+      for (int j = k % p; j + k < P; j += 2 * k) {
+#pragma unroll
+        for (int i = 0; i < k; ++i) {
+          if (i + j + k < P && (i + j) / (2 * p) == (i + j + k) / (2 * p)) {
+            T x = a[i + j], y = a[i + j + k];
+            a[i + j] = x < y ? x : y;
+            a[i + j + k] = x < y ? y : x;
+          }
+        }
+      }
+    }
+  }
+}
+
+template <int N>
+struct Pow2 {
+  static constexpr int v = N <= 1 ? 1 : N <= 2 ? 2 : N <= 4 ? 4 : N <= 8 ? 8 : 16;
+};
+
+// --------------------------------------------- exact moment comparisons ----
+// Moments of one histogram: count, exact sum and sum of squares.
+struct Mom {
+  uint64_t s1, s2;
+  uint32_t cnt;
+};
+
+struct U128 {
+  uint64_t hi, lo;
+};
+__device__ __forceinline__ U128 mul64(uint64_t a, uint64_t b) { return U128{__umul64hi(a, b), a * b}; }
+__device__ __forceinline__ bool lt128(U128 a, U128 b) { return a.hi < b.hi || (a.hi == b.hi && a.lo < b.lo); }
+__device__ __forceinline__ U128 sub128(U128 a, U128 b) {
+  return U128{a.hi - b.hi - (a.lo < b.lo ? 1ull : 0ull), a.lo - b.lo};
+}
+__device__ __forceinline__ U128 shr128(U128 a, int s) {
+  return U128{a.hi >> s, (a.lo >> s) | (a.hi << (64 - s))};
+}
+
+// V = count * sum(x^2) - sum(x)^2 = count * (count-1) * variance (exact).
+__device__ __forceinline__ uint64_t mom_v(const Mom& m) { return (uint64_t)m.cnt * m.s2 - m.s1 * m.s1; }
+// Histogram::cov (histogram.rs:193-197) is NaN when count <= 1 (0/0 variance)
+// or when the mean is 0 (0/0).
+__device__ __forceinline__ bool cov_nan(const Mom& m) { return m.cnt <= 1 || m.s1 == 0; }
+
+enum { CMP_LT = -1, CMP_EQ = 0, CMP_GT = 1, CMP_AMBIG = 2 };
+
+// Compare the reference's f64 COV of two histograms from exact moments.
+// The reference's computed COV carries a relative error below ~1e-14
+// (DESIGN.md "Exactness"); exact COV^2 ratios that differ by more than 2^-30
+// relative therefore order the same way in f64.  Closer calls return
+// CMP_AMBIG and the caller replays the reference arithmetic.
+__device__ __forceinline__ int cov_cmp(const Mom& a, const Mom& b) {
+  bool an = cov_nan(a), bn = cov_nan(b);
+  if (an || bn) return (an && bn) ? CMP_EQ : (an ? CMP_GT : CMP_LT);
+  uint64_t va = mom_v(a), vb = mom_v(b);
+  if (va == 0 && vb == 0) return CMP_EQ;  // both exactly 0.0
+  U128 x = mul64(va, b.s1 * b.s1), y = mul64(vb, a.s1 * a.s1);
+  bool xl = lt128(x, y);
+  U128 big = xl ? y : x, diff = xl ? sub128(y, x) : sub128(x, y);
+  U128 tol = shr128(big, 30);
+  if (!lt128(tol, diff)) return CMP_AMBIG;
+  return xl ? CMP_LT : CMP_GT;
+}
+
+// Histogram::mean (histogram.rs:172-181): exact sum / count, one rounding.
+__device__ __forceinline__ double mom_mean(const Mom& m) { return (double)m.s1 / (double)m.cnt; }
+// COV from exact moments (sqrt(V / (c (c-1))) / mean): within a few ulp of the
+// reference value; used for outputs, not for decisions.
+__device__ __forceinline__ double mom_cov(const Mom& m) {
+  double c = (double)m.cnt;
+  double var = (double)mom_v(m) / (c * (c - 1.0));
+  double mean = (double)m.s1 / c;
+  return sqrt(var) / mean;
+}
+
+// ------------------------------------------- reference-exact f64 replay ----
+// The reference computes variance as an ordered sum over DISTINCT values
+// ascending of ((mean - x)^2 * count) (histogram.rs:204-219).  `gen(i)`
+// yields the i-th of `cnt` values; distinct values are visited by repeated
+// min-above scans (O(cnt * distinct)); only near-tie decisions come here.
+template <class Gen>
+__device__ __forceinline__ double ref_variance_sum(const Gen& gen, uint32_t cnt, double mean) {
+  double sum = 0.0;
+  uint32_t lo = 0;
+  bool first = true;
+  for (;;) {
+    uint32_t x = 0xFFFFFFFFu, c = 0;
+    for (uint32_t i = 0; i < cnt; ++i) {
+      uint32_t v = gen(i);
+      if (!first && v < lo) continue;
+      if (v < x) {
+        x = v;
+        c = 1;
+      } else if (v == x) {
+        ++c;
+      }
+    }
+    if (c == 0) break;
+    double d = mean - (double)x;
+    double t = d * d;
+    t = t * (double)c;
+    sum = sum + t;
+    if (x == 0xFFFFFFFFu) break;
+    lo = x + 1;
+    first = false;
+  }
+  return sum;
+}
+
+template <class Gen>
+__device__ __forceinline__ double ref_cov(const Gen& gen, uint32_t cnt, uint64_t s1) {
+  double c = (double)cnt;
+  double mean = (double)s1 / c;
+  double var = ref_variance_sum(gen, cnt, mean) / (c - 1.0);
+  return sqrt(var) / mean;
+}
+
+template <class Gen>
+__device__ __forceinline__ double ref_mdtm(const Gen& gen, uint32_t cnt, uint64_t s1) {
+  double c = (double)cnt;
+  double mean = (double)s1 / c;
+  double sum = 0.0;
+  uint32_t lo = 0;
+  bool first = true;
+  for (;;) {
+    uint32_t x = 0xFFFFFFFFu, k = 0;
+    for (uint32_t i = 0; i < cnt; ++i) {
+      uint32_t v = gen(i);
+      if (!first && v < lo) continue;
+      if (v < x) {
+        x = v;
+        k = 1;
+      } else if (v == x) {
+        ++k;
+      }
+    }
+    if (k == 0) break;
+    double d = mean - (double)x;
+    sum = sum + fabs(d) * (double)k;
+    if (x == 0xFFFFFFFFu) break;
+    lo = x + 1;
+    first = false;
+  }
+  return sum / c;
+}
+
+// --------------------------------------------------------- top-K records --
+struct Rec {
+  uint64_t key, rank;
+};
+__device__ __forceinline__ bool rec_lt(const Rec& a, const Rec& b) {
+  return a.key < b.key || (a.key == b.key && a.rank < b.rank);
+}
+__device__ __forceinline__ Rec rec_max() { return Rec{~0ull, ~0ull}; }
+
+// In-LDS bitonic sort of a[0..n), n a power of two, by the whole block.
+__device__ inline void block_bitonic(Rec* a, int n) {
+  for (int k = 2; k <= n; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        int l = i ^ j;
+        if (l > i) {
+          Rec x = a[i], y = a[l];
+          bool up = (i & k) == 0;
+          if (up ? rec_lt(y, x) : rec_lt(x, y)) {
+            a[i] = y;
+            a[l] = x;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+}  // namespace bote

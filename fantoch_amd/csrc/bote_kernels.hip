@@ -1,0 +1,796 @@
+// bote_kernels.hip — gfx950 kernels for fantoch_bote's configuration search.
+//
+// Work mapping (DESIGN.md "Kernels"): one LANE evaluates one configuration at a
+// time; a wavefront holds 64 neighbouring configurations (colex-consecutive
+// ranks), so every per-client step is wave-uniform in the client and
+// lane-varying only in the config's members.  The R x R latency matrix (stored
+// latency << 4) and the client row offsets live in LDS; per-lane quorum tables
+// live in an LDS plane indexed [member][lane] (bank-conflict free).
+//
+// Reference map:
+//   eval_config            Search::compute_stats   fantoch_bote/src/search.rs:262-319
+//     Q phase              Bote::quorum_latency    fantoch_bote/src/lib.rs:155-163,169-185
+//     leader selection     Bote::best_leader (COV) fantoch_bote/src/lib.rs:99-150
+//     client loop          Bote::leaderless        fantoch_bote/src/lib.rs:38-59
+//     FPaxos moments       Bote::leader            fantoch_bote/src/lib.rs:67-89
+//     score / validity     Search::compute_score   fantoch_bote/src/search.rs:421-472
+//   rank enumeration       Search::compute_configs fantoch_bote/src/search.rs:234-260
+//                          (permutator combination -> colex ranks)
+//   k_single_*             Bote::{leaderless, leader, all_leaders_stats, best_leader}
+#include "bote_kernels.hpp"
+
+namespace bote {
+
+// ------------------------------------------------------------ LDS carving --
+struct Smem {
+  uint32_t* mat;     // R*R   latency << 4, row = from
+  uint32_t* clioff;  // nc    client row offsets (cli[c] * R)
+  uint32_t* srv;     // ns    server region ids
+  uint64_t* cs;      // 2*ns  per position: sum_c L[c][srv[p]], sum_c L^2
+  uint64_t* binom;   // (ns+1)*(N+1)
+  uint32_t* qtab;    // N * BD * NLW
+  Rec* top;          // MAXOBJ * KP
+  Rec* cand;         // BD
+  Rec* tmp;          // KP
+  Rec* thr;          // MAXOBJ
+  int* cnt;
+};
+
+__host__ __device__ inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+// One layout function used by host (sizing) and device (carving).
+__host__ __device__ inline size_t smem_layout(const EvalArgs& a, int N, int NLW, uint32_t BD, bool topk,
+                                              size_t* off) {
+  size_t o = 0;
+  off[0] = o; o += (size_t)a.R * a.R * 4;
+  off[1] = o; o += (size_t)a.nc * 4;
+  off[2] = o; o += (size_t)a.ns * 4;
+  o = align_up(o, 16);
+  off[3] = o; o += (size_t)a.ns * 16;
+  off[4] = o; o += a.cfgs ? 0 : (size_t)(a.ns + 1) * (N + 1) * 8;
+  o = align_up(o, 16);
+  off[5] = o; o += (size_t)N * BD * NLW * 4;
+  o = align_up(o, 16);
+  off[6] = o; o += topk ? (size_t)MAXOBJ * KP * 16 : 0;
+  off[7] = o; o += topk ? (size_t)BD * 16 : 0;
+  off[8] = o; o += topk ? (size_t)KP * 16 : 0;
+  off[9] = o; o += topk ? (size_t)MAXOBJ * 16 : 0;
+  off[10] = o; o += 16;
+  return o;
+}
+
+template <int N>
+__device__ inline Smem carve(const EvalArgs& a, unsigned char* base, int NLW) {
+  size_t off[11];
+  smem_layout(a, N, NLW, blockDim.x, a.out_top != nullptr, off);
+  Smem s;
+  s.mat = (uint32_t*)(base + off[0]);
+  s.clioff = (uint32_t*)(base + off[1]);
+  s.srv = (uint32_t*)(base + off[2]);
+  s.cs = (uint64_t*)(base + off[3]);
+  s.binom = (uint64_t*)(base + off[4]);
+  s.qtab = (uint32_t*)(base + off[5]);
+  s.top = (Rec*)(base + off[6]);
+  s.cand = (Rec*)(base + off[7]);
+  s.tmp = (Rec*)(base + off[8]);
+  s.thr = (Rec*)(base + off[9]);
+  s.cnt = (int*)(base + off[10]);
+  return s;
+}
+
+// arr[i] for a lane-varying i without an indexed private array: an OR of
+// masked registers (a plain select chain is turned into a scratch lookup).
+template <int N>
+__device__ __forceinline__ uint32_t sel(const uint32_t (&arr)[N], uint32_t i) {
+  uint32_t r = 0;
+#pragma unroll
+  for (int j = 0; j < N; ++j) r |= arr[j] & (0u - (uint32_t)(i == (uint32_t)j));
+  return r;
+}
+
+// ----------------------------------------------------- colex enumeration --
+// rank = sum_j C(p_j, j+1) with p ascending (an extension: the reference's
+// permutator order is not pinned).
+template <int N>
+__device__ __forceinline__ void colex_unrank(const uint64_t* binom, uint32_t ns, uint64_t rank, uint32_t (&p)[N]) {
+  uint64_t r = rank;
+  uint32_t hi = ns;
+#pragma unroll
+  for (int j = N - 1; j >= 0; --j) {
+    const uint32_t k = j + 1;
+    uint32_t lo = j, up = hi;  // answer in [lo, up)
+    while (up - lo > 1) {
+      uint32_t mid = (lo + up) >> 1;
+      if (binom[mid * (N + 1) + k] <= r) lo = mid; else up = mid;
+    }
+    p[j] = lo;
+    r -= binom[lo * (N + 1) + k];
+    hi = lo;
+  }
+}
+
+template <int N>
+__device__ __forceinline__ void colex_next(uint32_t ns, uint32_t (&p)[N]) {
+  uint32_t js = N;  // first j with p[j] + 1 < p[j+1]
+#pragma unroll
+  for (int j = N - 1; j >= 0; --j) {
+    uint32_t nxt = (j == N - 1) ? ns : p[j + 1];
+    if (p[j] + 1 < nxt) js = j;
+  }
+#pragma unroll
+  for (int j = 0; j < N; ++j) p[j] = (uint32_t)j < js ? (uint32_t)j : ((uint32_t)j == js ? p[j] + 1 : p[j]);
+}
+
+// --------------------------------------------------------- config result --
+struct CfgOut {
+  Mom mom[NSLOT];
+  uint32_t lead_orig;
+  double score;
+  bool valid;
+};
+
+// Slot presence for a config of size N (af2/ff2 need max_f >= 2).
+template <int N>
+__device__ __forceinline__ bool slot_has(int s) {
+  int b = s % 5;
+  return !((b == SLOT_AF2 || b == SLOT_FF2) && QCfg<N>::maxf < 2);
+}
+
+// ------------------------------------------------------------- eval one ---
+// Evaluate the configuration whose members are positions p[0..N) of the
+// server list (given order = config order).  `oi` is the output row (FULL).
+template <int N, bool FULL>
+__device__ __forceinline__ void eval_config(const EvalArgs& a, const Smem& s, const uint32_t (&p)[N], bool sorted_in, uint64_t oi,
+                            CfgOut& out) {
+  using QC = QCfg<N>;
+  constexpr int NL = QC::NL;
+  constexpr int P = Pow2<N>::v;
+  const uint32_t BD = blockDim.x, tid = threadIdx.x;
+  const uint32_t R = a.R, nc = a.nc;
+
+  // --- members, sorted by region id (== name order) for the closest-server
+  //     tie-break; `orig` keeps the config order for the leader tie-break.
+  uint32_t mk[P];
+#pragma unroll
+  for (int j = 0; j < N; ++j) mk[j] = (s.srv[p[j]] << 12) | (p[j] << 4) | (uint32_t)j;
+#pragma unroll
+  for (int j = N; j < P; ++j) mk[j] = 0xFFFFFFFFu;
+  if (!sorted_in) sort_network<P>(mk);
+  uint32_t mreg[N], mpos[N], morig[N], moff[N];
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    mreg[j] = mk[j] >> 12;
+    mpos[j] = (mk[j] >> 4) & 0xFF;
+    morig[j] = mk[j] & 15;
+    moff[j] = mreg[j] * R;
+  }
+
+  // --- Q phase: per member j, the sorted distances to the config (row j of
+  //     the config submatrix, self included); colocated closest server.
+  uint32_t Qf1[N], Qf2[N], Ql[NL][N], cdk[N];
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    uint32_t v[P];
+    uint32_t key = 0xFFFFFFFFu;
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+      uint32_t w = s.mat[moff[j] + mreg[k]];
+      v[k] = w >> LAT_SHIFT;
+      key = min(key, w | (uint32_t)k);
+    }
+#pragma unroll
+    for (int k = N; k < P; ++k) v[k] = 0xFFFFFFFFu;
+    sort_network<P>(v);
+    Qf1[j] = v[QC::qf1 - 1];
+    Qf2[j] = QC::maxf >= 2 ? v[(QC::maxf >= 2 ? QC::qf2 : 1) - 1] : 0;
+#pragma unroll
+    for (int t = 0; t < NL; ++t) Ql[t][j] = v[QC::lq(t) - 1];
+    cdk[j] = key;
+    if (NL <= 2) {
+      uint32_t w = Ql[0][j] | (NL == 2 ? (Ql[NL - 1][j] << 16) : 0u);
+      s.qtab[j * BD + tid] = w;
+    } else {
+      uint2 w;
+      w.x = Ql[0][j] | (Ql[1][j] << 16);
+      w.y = Ql[NL - 1][j];
+      ((uint2*)s.qtab)[j * BD + tid] = w;
+    }
+  }
+
+  // --- FPaxos leader: min COV over the Input clients at f = 1 (q = 2),
+  //     first in config order on ties.  Exact moments from the per-position
+  //     column sums: sum_c (L[c][l] + Q)^k expands in sum_c L and sum_c L^2.
+  Mom lm[N];
+#pragma unroll
+  for (int l = 0; l < N; ++l) {
+    uint64_t c1 = s.cs[2 * mpos[l]], c2 = s.cs[2 * mpos[l] + 1], q = Qf1[l];
+    lm[l] = Mom{c1 + (uint64_t)nc * q, c2 + 2ull * q * c1 + (uint64_t)nc * q * q, nc};
+  }
+  Mom bm = lm[0];
+  uint32_t bo = morig[0], bi = 0;
+  bool amb = false;
+#pragma unroll
+  for (int l = 1; l < N; ++l) {
+    int c = cov_cmp(lm[l], bm);
+    if (c == CMP_AMBIG) {
+      amb = true;
+    } else if (c == CMP_LT || (c == CMP_EQ && morig[l] < bo)) {
+      bm = lm[l];
+      bo = morig[l];
+      bi = l;
+    }
+  }
+  if (amb) {
+    // Near-tie: replay the reference's f64 arithmetic for every leader.
+    double cv[N];
+#pragma unroll
+    for (int l = 0; l < N; ++l) {
+      const uint32_t col = mreg[l], q = Qf1[l];
+      auto gen = [&](uint32_t c) { return (s.mat[s.clioff[c] + col] >> LAT_SHIFT) + q; };
+      cv[l] = ref_cov(gen, nc, lm[l].s1);
+    }
+    double bc = cv[0];
+    bo = morig[0];
+    bi = 0;
+#pragma unroll
+    for (int l = 1; l < N; ++l) {
+      int c = f64_cmp(cv[l], bc);
+      if (c < 0 || (c == 0 && morig[l] < bo)) {
+        bc = cv[l];
+        bo = morig[l];
+        bi = l;
+      }
+    }
+  }
+  const uint32_t lreg = sel(mreg, bi), lpos = sel(mpos, bi);
+  const uint32_t lq1 = sel(Qf1, bi), lq2 = sel(Qf2, bi);
+  out.lead_orig = bo;
+
+  const uint32_t stride = 5 * nc + 5 * N;
+  const bool wv = FULL && a.out_vals != nullptr;  // write per-client values
+  uint32_t* ov = wv ? a.out_vals + oi * stride : nullptr;
+
+  // --- Input FPaxos (search.rs:291-302): moments from column sums.
+  {
+    uint64_t c1 = s.cs[2 * lpos], c2 = s.cs[2 * lpos + 1];
+    uint64_t q = lq1;
+    out.mom[SLOT_FF1] = Mom{c1 + (uint64_t)nc * q, c2 + 2ull * q * c1 + (uint64_t)nc * q * q, nc};
+    q = lq2;
+    out.mom[SLOT_FF2] = Mom{c1 + (uint64_t)nc * q, c2 + 2ull * q * c1 + (uint64_t)nc * q * q, nc};
+  }
+
+  // --- Colocated keys: clients are the config members (config order).
+  {
+    uint64_t f1 = 0, f1s = 0, f2 = 0, f2s = 0;
+    uint64_t l1[NL], l2[NL];
+#pragma unroll
+    for (int t = 0; t < NL; ++t) l1[t] = l2[t] = 0;
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+      uint32_t v = s.mat[moff[k] + lreg] >> LAT_SHIFT;  // ping_latency(client k, leader)
+      uint32_t x1 = v + lq1, x2 = v + lq2;
+      f1 += x1; f1s += (uint64_t)x1 * x1;
+      f2 += x2; f2s += (uint64_t)x2 * x2;
+      uint32_t d = cdk[k] >> LAT_SHIFT, js = cdk[k] & 15;
+      uint32_t A[NL];
+#pragma unroll
+      for (int t = 0; t < NL; ++t) {
+        A[t] = d + sel(Ql[t], js);
+        l1[t] += A[t];
+        l2[t] += (uint64_t)A[t] * A[t];
+      }
+      if (wv) {
+        uint32_t* oc = ov + 5 * nc;
+        uint32_t o = morig[k];
+        oc[SLOT_AF1 * N + o] = A[QC::idx_a1];
+        oc[SLOT_FF1 * N + o] = x1;
+        oc[SLOT_AF2 * N + o] = QC::maxf >= 2 ? A[QC::idx_a2] : 0xFFFFFFFFu;
+        oc[SLOT_FF2 * N + o] = QC::maxf >= 2 ? x2 : 0xFFFFFFFFu;
+        oc[SLOT_E * N + o] = A[QC::idx_e];
+      }
+    }
+    out.mom[5 + SLOT_FF1] = Mom{f1, f1s, (uint32_t)N};
+    out.mom[5 + SLOT_FF2] = Mom{f2, f2s, (uint32_t)N};
+    out.mom[5 + SLOT_AF1] = Mom{l1[QC::idx_a1], l2[QC::idx_a1], (uint32_t)N};
+    out.mom[5 + SLOT_AF2] = Mom{l1[QC::idx_a2], l2[QC::idx_a2], (uint32_t)N};
+    out.mom[5 + SLOT_E] = Mom{l1[QC::idx_e], l2[QC::idx_e], (uint32_t)N};
+  }
+
+  // --- Input leaderless: the hot loop.  Per client (wave-uniform): the
+  //     nearest member by packed (latency << 4 | member) min, then the
+  //     member's quorum latencies from the lane's LDS table.
+  {
+    uint32_t S1[NL];
+    uint64_t S2[NL];
+#pragma unroll
+    for (int t = 0; t < NL; ++t) { S1[t] = 0; S2[t] = 0; }
+    for (uint32_t c = 0; c < nc; ++c) {
+      const uint32_t off = s.clioff[c];
+      uint32_t m = 0xFFFFFFFFu;
+#pragma unroll
+      for (int k = 0; k < N; ++k) m = min(m, s.mat[off + mreg[k]] | (uint32_t)k);
+      const uint32_t js = m & 15, d = m >> LAT_SHIFT;
+      uint32_t A[NL];
+      if (NL <= 2) {
+        uint32_t w = s.qtab[js * BD + tid];
+        A[0] = d + (w & 0xFFFF);
+        if (NL == 2) A[NL - 1] = d + (w >> 16);
+      } else {
+        uint2 w = ((const uint2*)s.qtab)[js * BD + tid];
+        A[0] = d + (w.x & 0xFFFF);
+        A[1] = d + (w.x >> 16);
+        A[NL - 1] = d + w.y;
+      }
+#pragma unroll
+      for (int t = 0; t < NL; ++t) {
+        S1[t] += A[t];
+        S2[t] += (uint64_t)A[t] * A[t];
+      }
+      if (wv) {
+        uint32_t v = s.mat[off + lreg] >> LAT_SHIFT;
+        ov[SLOT_AF1 * nc + c] = A[QC::idx_a1];
+        ov[SLOT_FF1 * nc + c] = v + lq1;
+        ov[SLOT_AF2 * nc + c] = QC::maxf >= 2 ? A[QC::idx_a2] : 0xFFFFFFFFu;
+        ov[SLOT_FF2 * nc + c] = QC::maxf >= 2 ? v + lq2 : 0xFFFFFFFFu;
+        ov[SLOT_E * nc + c] = A[QC::idx_e];
+      }
+    }
+    out.mom[SLOT_AF1] = Mom{S1[QC::idx_a1], S2[QC::idx_a1], nc};
+    out.mom[SLOT_AF2] = Mom{S1[QC::idx_a2], S2[QC::idx_a2], nc};
+    out.mom[SLOT_E] = Mom{S1[QC::idx_e], S2[QC::idx_e], nc};
+  }
+
+  // --- Search::compute_score (search.rs:421-472), bit-exact.
+  out.valid = false;
+  out.score = 0.0;
+  if (a.want_score) {
+    const int fmax = min(N / 2, a.ft_metric);
+    bool valid = true;
+    double score = 0.0;
+#pragma unroll
+    for (int f = 1; f <= 2; ++f) {
+      if (f > fmax) break;
+      const int sa = f == 1 ? SLOT_AF1 : SLOT_AF2, sf = f == 1 ? SLOT_FF1 : SLOT_FF2;
+      const Mom& ma = out.mom[sa];
+      const Mom& mf = out.mom[sf];
+      double fmi = mom_mean(mf) - mom_mean(ma);
+      bool fair;
+      if (cov_nan(mf) || cov_nan(ma)) {
+        fair = false;  // NaN - x >= p is false
+      } else {
+        int c = CMP_AMBIG;
+        if (a.p_fair == 0.0) {
+          c = cov_cmp(mf, ma);
+          fair = c != CMP_LT;
+        } else {
+          double d = mom_cov(mf) - mom_cov(ma);
+          double tol = 1e-9 * (1.0 + fabs(mom_cov(mf)) + fabs(mom_cov(ma)));
+          if (fabs(d - a.p_fair) > tol) c = CMP_EQ;
+          fair = d >= a.p_fair;
+        }
+        if (c == CMP_AMBIG) {
+          // replay the reference's f64 covs of ff_f and af_f (Input)
+          const uint32_t qfl = f == 1 ? lq1 : lq2;
+          auto genf = [&](uint32_t cc) { return (s.mat[s.clioff[cc] + lreg] >> LAT_SHIFT) + qfl; };
+          const int ti = f == 1 ? QC::idx_a1 : QC::idx_a2;
+          auto gena = [&](uint32_t cc) {
+            const uint32_t off = s.clioff[cc];
+            uint32_t m = 0xFFFFFFFFu;
+#pragma unroll
+            for (int k = 0; k < N; ++k) m = min(m, s.mat[off + mreg[k]] | (uint32_t)k);
+            uint32_t js = m & 15;
+            uint32_t q = 0;
+#pragma unroll
+            for (int t = 0; t < NL; ++t)
+              if (t == ti) q = sel(Ql[t], js);
+            return (m >> LAT_SHIFT) + q;
+          };
+          double cf = ref_cov(genf, nc, mf.s1), ca = ref_cov(gena, nc, ma.s1);
+          fair = (cf - ca) >= a.p_fair;
+        }
+      }
+      valid = valid && fmi >= a.p_fmean && fair;
+      double emi = mom_mean(out.mom[SLOT_E]) - mom_mean(ma);
+      if (N == 11 || N == 13) valid = valid && emi >= a.p_emean;
+      double t = 30.0 * emi;
+      t = fmi + t;
+      score = score + t;
+    }
+    out.valid = valid;
+    out.score = score;
+  }
+}
+
+// ----------------------------------------------------- block top-K (LDS) --
+__device__ inline int lower_bound_rec(const Rec* a, int n, const Rec& x) {
+  int lo = 0, hi = n;
+  while (lo < hi) {
+    int mid = (lo + hi) >> 1;
+    if (rec_lt(a[mid], x)) lo = mid + 1; else hi = mid;
+  }
+  return lo;
+}
+__device__ inline int upper_bound_rec(const Rec* a, int n, const Rec& x) {
+  int lo = 0, hi = n;
+  while (lo < hi) {
+    int mid = (lo + hi) >> 1;
+    if (!rec_lt(x, a[mid])) lo = mid + 1; else hi = mid;
+  }
+  return lo;
+}
+
+// Merge the block's candidate buffer (s.cnt entries) into objective o's list.
+__device__ void topk_merge(const Smem& s, int o, uint32_t K) {
+  const int BD = blockDim.x, tid = threadIdx.x;
+  const int n = *s.cnt;
+  if (tid >= n) s.cand[tid] = rec_max();
+  __syncthreads();
+  block_bitonic(s.cand, BD);
+  Rec* top = s.top + o * KP;
+  if (tid < KP) {
+    Rec x = top[tid];
+    int r = tid + lower_bound_rec(s.cand, BD, x);
+    if (r < KP) s.tmp[r] = x;
+  }
+  {
+    Rec y = s.cand[tid];
+    int r = tid + upper_bound_rec(top, KP, y);
+    if (r < KP) s.tmp[r] = y;
+  }
+  __syncthreads();
+  if (tid < KP) top[tid] = s.tmp[tid];
+  __syncthreads();
+  if (tid == 0) {
+    s.thr[o] = top[K - 1];
+    *s.cnt = 0;
+  }
+  __syncthreads();
+}
+
+// ------------------------------------------------------------ the kernel --
+template <int N, bool FULL>
+__global__ void __launch_bounds__(256) eval_kernel(EvalArgs a) {
+  using QC = QCfg<N>;
+  constexpr int NLW = QC::NL <= 2 ? 1 : 2;
+  extern __shared__ __align__(16) unsigned char smem[];
+  const Smem s = carve<N>(a, smem, NLW);
+  const uint32_t BD = blockDim.x, tid = threadIdx.x;
+  const bool topk = !FULL && a.out_top != nullptr;
+
+  // stage the planet, client offsets, server list, column sums, binomials
+  for (uint32_t i = tid; i < a.R * a.R; i += BD) s.mat[i] = a.mat[i];
+  for (uint32_t i = tid; i < a.nc; i += BD) s.clioff[i] = a.cli[i] * a.R;
+  for (uint32_t i = tid; i < a.ns; i += BD) s.srv[i] = a.srv[i];
+  if (!a.cfgs)
+    for (uint32_t i = tid; i < (a.ns + 1) * (N + 1); i += BD) s.binom[i] = a.binom[i];
+  if (topk) {
+    for (uint32_t i = tid; i < MAXOBJ * KP; i += BD) s.top[i] = rec_max();
+    if (tid < MAXOBJ) s.thr[tid] = rec_max();
+    if (tid == 0) *s.cnt = 0;
+  }
+  __syncthreads();
+  for (uint32_t i = tid; i < a.ns; i += BD) {
+    uint64_t c1 = 0, c2 = 0;
+    const uint32_t col = s.srv[i];
+    for (uint32_t c = 0; c < a.nc; ++c) {
+      uint64_t v = s.mat[s.clioff[c] + col] >> LAT_SHIFT;
+      c1 += v;
+      c2 += v * v;
+    }
+    s.cs[2 * i] = c1;
+    s.cs[2 * i + 1] = c2;
+  }
+  __syncthreads();
+
+  const uint64_t total = a.re - a.rb;
+  const uint64_t runlen = a.runlen;
+  const uint64_t njobs = (total + runlen - 1) / runlen;
+  const uint64_t G = (uint64_t)gridDim.x * BD;
+  const uint64_t outer = (njobs + G - 1) / G;
+  const bool sorted_in = !a.cfgs && a.srv_sorted;
+  uint64_t valid_cnt = 0, digest = 0;
+
+  for (uint64_t it = 0; it < outer; ++it) {
+    const uint64_t job = it * G + (uint64_t)blockIdx.x * BD + tid;
+    const bool jobok = job < njobs;
+    uint64_t rank = a.rb + job * runlen;  // rank or config index
+    uint32_t p[N];
+#pragma unroll
+    for (int j = 0; j < N; ++j) p[j] = j;
+    if (jobok) {
+      if (a.cfgs) {
+#pragma unroll
+        for (int j = 0; j < N; ++j) p[j] = a.cfgs[rank * N + j];
+      } else {
+        colex_unrank<N>(s.binom, a.ns, rank, p);
+      }
+    }
+    for (uint64_t t = 0; t < runlen; ++t) {
+      const bool have = jobok && rank < a.re;
+      CfgOut r;
+      if (have) {
+        eval_config<N, FULL>(a, s, p, sorted_in, rank - a.rb, r);
+        if (r.valid) ++valid_cnt;
+        if (a.want_digest) {
+          uint64_t h = mix64(rank ^ ((uint64_t)r.lead_orig << 56));
+#pragma unroll
+          for (int sl = 0; sl < NSLOT; ++sl) {
+            if (!slot_has<N>(sl)) continue;
+            h = mix64(h ^ (r.mom[sl].s1 + ((uint64_t)sl << 48)));
+            h = mix64(h ^ r.mom[sl].s2);
+          }
+          digest += h;
+        }
+        if (FULL) {
+          const uint64_t oi = rank - a.rb;
+          if (a.out_leader) a.out_leader[oi] = r.lead_orig;
+#pragma unroll
+          for (int sl = 0; sl < NSLOT; ++sl) {
+            const bool h = slot_has<N>(sl);
+            if (a.out_s1) a.out_s1[oi * NSLOT + sl] = h ? r.mom[sl].s1 : ~0ull;
+            if (a.out_s2) a.out_s2[oi * NSLOT + sl] = h ? r.mom[sl].s2 : ~0ull;
+            if (a.out_mean) a.out_mean[oi * NSLOT + sl] = h ? mom_mean(r.mom[sl]) : __longlong_as_double(0x7FF8000000000000ll);
+            if (a.out_cov) a.out_cov[oi * NSLOT + sl] = h ? mom_cov(r.mom[sl]) : __longlong_as_double(0x7FF8000000000000ll);
+          }
+          if (a.out_score) a.out_score[oi] = r.score;
+          if (a.out_valid) a.out_valid[oi] = r.valid ? 1 : 0;
+        }
+      }
+      if (topk) {
+        uint64_t key[MAXOBJ];
+        bool pass[MAXOBJ];
+        bool any = false;
+#pragma unroll
+        for (int o = 0; o < MAXOBJ; ++o) {
+          pass[o] = false;
+          key[o] = 0;
+          if (o < a.n_obj && have) {
+            const uint32_t kind = a.obj_kind[o], sl = a.obj_slot[o];
+            bool ok = true;
+            if (kind == OBJ_SCORE) {
+              ok = r.valid;
+              key[o] = ~orderable_f64(r.score);
+            } else {
+              // `sl` is uniform: one scalar branch per slot keeps r.mom in
+              // registers (a select chain here gets turned into scratch).
+#pragma unroll
+              for (int q = 0; q < NSLOT; ++q) {
+                if ((uint32_t)q == sl) {
+                  const Mom& m = r.mom[q];
+                  if (kind == OBJ_MEAN) {
+                    key[o] = m.s1;
+                  } else if (cov_nan(m)) {
+                    key[o] = ~0ull;
+                  } else {
+                    double rr = (double)mom_v(m) / ((double)m.s1 * (double)m.s1);
+                    key[o] = (uint64_t)__double_as_longlong(rr);
+                  }
+                }
+              }
+            }
+            pass[o] = ok && rec_lt(Rec{key[o], rank}, s.thr[o]);
+            any = any || pass[o];
+          }
+        }
+        if (__syncthreads_or(any)) {
+#pragma unroll
+          for (int o = 0; o < MAXOBJ; ++o) {
+            if (o >= a.n_obj) break;
+            if (pass[o] && rec_lt(Rec{key[o], rank}, s.thr[o])) {
+              int i = atomicAdd(s.cnt, 1);
+              s.cand[i] = Rec{key[o], rank};
+            }
+            __syncthreads();
+            if (*s.cnt > 0) topk_merge(s, o, a.K);
+          }
+        }
+      }
+      if (have && !a.cfgs) colex_next<N>(a.ns, p);
+      ++rank;
+    }
+  }
+
+  if (a.out_counters) {
+    if (valid_cnt) atomicAdd(&a.out_counters[0], (unsigned long long)valid_cnt);
+    if (digest) atomicAdd(&a.out_counters[1], (unsigned long long)digest);
+  }
+  if (topk) {
+    __syncthreads();
+    Rec* dst = a.out_top + (size_t)blockIdx.x * a.n_obj * KP;
+    for (uint32_t i = tid; i < (uint32_t)a.n_obj * KP; i += BD) dst[i] = s.top[i];
+  }
+}
+
+// ----------------------------------------------------- top-K list merge --
+// lists: n_lists lists, list i of objective o at src[i * list_stride + o * KP]
+// out:   one list per group of G_MERGE_LISTS lists, at dst[g * out_stride + o * KP]
+__global__ void __launch_bounds__(256) merge_kernel(const Rec* src, uint32_t n_lists, uint64_t list_stride, Rec* dst,
+                                                     uint64_t out_stride) {
+  __shared__ Rec buf[G_MERGE_LISTS * KP];
+  const uint32_t g = blockIdx.x, o = blockIdx.y;
+  for (uint32_t i = threadIdx.x; i < G_MERGE_LISTS * KP; i += blockDim.x) {
+    uint32_t l = g * G_MERGE_LISTS + i / KP;
+    buf[i] = l < n_lists ? src[l * list_stride + o * KP + i % KP] : rec_max();
+  }
+  __syncthreads();
+  block_bitonic(buf, G_MERGE_LISTS * KP);
+  for (uint32_t i = threadIdx.x; i < KP; i += blockDim.x) dst[g * out_stride + o * KP + i] = buf[i];
+}
+
+// ------------------------------------------------- single-config kernels --
+// Shared by Bote::{leaderless, leader, all_leaders_stats, best_leader}.
+// Server membership is a set (the reference filters with `contains`).
+
+
+// q-th closest (1-based) from row `from` over the member set: counting
+// selection, O(R) per call over the set members in (latency, id) order.
+__device__ inline uint32_t quorum_lat(const uint32_t* smat, const uint8_t* member, uint32_t R, uint32_t from, uint32_t q,
+                                      int* err) {
+  // the q-th smallest of { L[from][t] : member[t] } (ties irrelevant for the value)
+  for (uint32_t t = 0; t < R; ++t) {
+    if (!member[t]) continue;
+    uint32_t v = smat[from * R + t] >> LAT_SHIFT;
+    uint32_t lt = 0, le = 0;
+    for (uint32_t u = 0; u < R; ++u) {
+      if (!member[u]) continue;
+      uint32_t w = smat[from * R + u] >> LAT_SHIFT;
+      lt += w < v;
+      le += w <= v;
+    }
+    if (lt < q && q <= le) return v;
+  }
+  if (err) *err = 1;
+  return 0;
+}
+
+__device__ inline uint32_t closest_member(const uint32_t* smat, const uint8_t* member, uint32_t R, uint32_t from) {
+  // packed (latency << 8 | id) min: the (latency, name) order with id == name rank
+  uint32_t key = 0xFFFFFFFFu;
+  for (uint32_t t = 0; t < R; ++t)
+    if (member[t]) key = min(key, ((smat[from * R + t] >> LAT_SHIFT) << 8) | t);
+  return key;
+}
+
+// mode 0: quorum latencies of `froms`; 1: leaderless; 2: leader; 3: all leaders
+__global__ void __launch_bounds__(256) single_kernel(SingleArgs a, int mode) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  uint32_t* smat = (uint32_t*)smem;
+  uint8_t* member = (uint8_t*)(smat + a.R * a.R);
+  uint32_t* qlat = (uint32_t*)(smem + align_up(a.R * a.R * 4 + a.R, 16));
+  for (uint32_t i = threadIdx.x; i < a.R * a.R; i += blockDim.x) smat[i] = a.mat[i];
+  for (uint32_t i = threadIdx.x; i < a.R; i += blockDim.x) member[i] = 0;
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < a.ns; i += blockDim.x) member[a.servers[i]] = 1;
+  __syncthreads();
+  // quorum latency of every region (only member rows are used)
+  for (uint32_t r = threadIdx.x; r < a.R; r += blockDim.x) qlat[r] = quorum_lat(smat, member, a.R, r, a.q, a.err);
+  __syncthreads();
+  if (mode == 0) {
+    for (uint32_t i = threadIdx.x; i < a.nf; i += blockDim.x) a.out[i] = qlat[a.froms[i]];
+  } else if (mode == 1) {
+    for (uint32_t i = threadIdx.x; i < a.nc; i += blockDim.x) {
+      uint32_t c = a.clients[i];
+      uint32_t key = closest_member(smat, member, a.R, c);
+      a.out[i] = (uint64_t)(key >> 8) + qlat[key & 0xFF];
+    }
+  } else if (mode == 2) {
+    for (uint32_t i = threadIdx.x; i < a.nc; i += blockDim.x) {
+      uint32_t c = a.clients[i];
+      a.out[i] = (uint64_t)(smat[c * a.R + a.leader] >> LAT_SHIFT) + qlat[a.leader];
+    }
+  } else {
+    for (uint32_t i = threadIdx.x; i < a.ns * a.nc; i += blockDim.x) {
+      uint32_t l = a.servers[i / a.nc], c = a.clients[i % a.nc];
+      a.out[i] = (uint64_t)(smat[c * a.R + l] >> LAT_SHIFT) + qlat[l];
+    }
+  }
+}
+
+// Bote::best_leader: one thread per leader computes the reference's f64 stat
+// (ordered sums), then thread 0 takes the first minimum under F64's order.
+__global__ void __launch_bounds__(256) best_leader_kernel(SingleArgs a, const uint64_t* vals, double* stat) {
+  for (uint32_t l = threadIdx.x; l < a.ns; l += blockDim.x) {
+    const uint64_t* v = vals + (size_t)l * a.nc;
+    uint64_t s1 = 0;
+    for (uint32_t c = 0; c < a.nc; ++c) s1 += v[c];
+    auto gen = [&](uint32_t c) { return (uint32_t)v[c]; };
+    double x;
+    if (a.stat == 0) x = (double)s1 / (double)a.nc;
+    else if (a.stat == 1) x = ref_cov(gen, a.nc, s1);
+    else x = ref_mdtm(gen, a.nc, s1);
+    stat[l] = x;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t b = 0;
+    for (uint32_t l = 1; l < a.ns; ++l)
+      if (f64_cmp(stat[l], stat[b]) < 0) b = l;
+    *a.out_pos = b;
+  }
+}
+
+// ------------------------------------------------------------- launchers --
+template <int N, bool FULL>
+static hipError_t launch_eval_n(const EvalArgs& a, uint32_t grid, uint32_t bd, size_t shm, hipStream_t st) {
+  auto k = eval_kernel<N, FULL>;
+  hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k, dim3(grid), dim3(bd), shm, st, a);
+  return hipGetLastError();
+}
+
+size_t eval_smem_bytes(const EvalArgs& a, uint32_t n, uint32_t bd, bool topk) {
+  size_t off[11];
+  int nl = 0;
+  switch (n) {
+#define NL_CASE(NN) case NN: nl = QCfg<NN>::NL; break;
+    NL_CASE(2) NL_CASE(3) NL_CASE(4) NL_CASE(5) NL_CASE(6) NL_CASE(7) NL_CASE(8) NL_CASE(9)
+    NL_CASE(10) NL_CASE(11) NL_CASE(12) NL_CASE(13) NL_CASE(14) NL_CASE(15) NL_CASE(16)
+#undef NL_CASE
+    default: return 0;
+  }
+  return smem_layout(a, (int)n, nl <= 2 ? 1 : 2, bd, topk, off);
+}
+
+int eval_occupancy(uint32_t n, bool full, uint32_t bd, size_t shm) {
+  int nb = 0;
+  const void* k = nullptr;
+  switch (n) {
+#define OCC_CASE(NN) case NN: k = full ? (const void*)eval_kernel<NN, true> : (const void*)eval_kernel<NN, false>; break;
+    OCC_CASE(2) OCC_CASE(3) OCC_CASE(4) OCC_CASE(5) OCC_CASE(6) OCC_CASE(7) OCC_CASE(8) OCC_CASE(9)
+    OCC_CASE(10) OCC_CASE(11) OCC_CASE(12) OCC_CASE(13) OCC_CASE(14) OCC_CASE(15) OCC_CASE(16)
+#undef OCC_CASE
+    default: return 0;
+  }
+  hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, (int)bd, shm) != hipSuccess) return 1;
+  return nb > 0 ? nb : 1;
+}
+
+hipError_t launch_eval(const EvalArgs& a, uint32_t n, bool full, uint32_t grid, uint32_t bd, size_t shm,
+                       hipStream_t st) {
+  switch (n) {
+#define EV_CASE(NN) \
+  case NN: return full ? launch_eval_n<NN, true>(a, grid, bd, shm, st) : launch_eval_n<NN, false>(a, grid, bd, shm, st);
+    EV_CASE(2) EV_CASE(3) EV_CASE(4) EV_CASE(5) EV_CASE(6) EV_CASE(7) EV_CASE(8) EV_CASE(9)
+    EV_CASE(10) EV_CASE(11) EV_CASE(12) EV_CASE(13) EV_CASE(14) EV_CASE(15) EV_CASE(16)
+#undef EV_CASE
+    default: return hipErrorInvalidValue;
+  }
+}
+
+hipError_t launch_merge(const Rec* src, uint32_t n_lists, uint64_t list_stride, Rec* dst, uint64_t out_stride,
+                        uint32_t n_obj, hipStream_t st) {
+  uint32_t groups = (n_lists + G_MERGE_LISTS - 1) / G_MERGE_LISTS;
+  hipLaunchKernelGGL(merge_kernel, dim3(groups, n_obj), dim3(256), 0, st, src, n_lists, list_stride, dst, out_stride);
+  return hipGetLastError();
+}
+
+__global__ void sum_counters_kernel(const uint64_t* src, uint32_t n, uint64_t stride, uint64_t off, uint64_t* dst) {
+  if (threadIdx.x < 2) {
+    uint64_t s = 0;
+    for (uint32_t i = 0; i < n; ++i) s += src[i * stride + off + threadIdx.x];
+    dst[threadIdx.x] = s;
+  }
+}
+
+hipError_t launch_sum_counters(const uint64_t* src, uint32_t n, uint64_t stride, uint64_t off, uint64_t* dst,
+                               hipStream_t st) {
+  hipLaunchKernelGGL(sum_counters_kernel, dim3(1), dim3(64), 0, st, src, n, stride, off, dst);
+  return hipGetLastError();
+}
+
+hipError_t launch_single(const SingleArgs& a, int mode, hipStream_t st) {
+  size_t shm = align_up((size_t)a.R * a.R * 4 + a.R, 16) + (size_t)a.R * 4;
+  hipError_t e = hipFuncSetAttribute((const void*)single_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(single_kernel, dim3(1), dim3(256), shm, st, a, mode);
+  return hipGetLastError();
+}
+
+hipError_t launch_best_leader(const SingleArgs& a, const uint64_t* vals, double* stat, hipStream_t st) {
+  hipLaunchKernelGGL(best_leader_kernel, dim3(1), dim3(256), 0, st, a, vals, stat);
+  return hipGetLastError();
+}
+
+}  // namespace bote

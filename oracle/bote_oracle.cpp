@@ -662,6 +662,24 @@ int oracle_compute_stats(void* h, const uint32_t* configs, uint32_t ncfg, uint32
   ORACLE_CATCH
 }
 
+// compute_score (search.rs:421-472) for a batch of explicit configs.
+int oracle_scores(void* h, const uint32_t* configs, uint32_t ncfg, uint32_t n, const uint32_t* clients,
+                  uint32_t nc, const double* rparams, int ft_metric, double* out_score, uint8_t* out_valid) {
+  ORACLE_TRY
+  Bote b{(Planet*)h};
+  std::vector<uint32_t> cl(clients, clients + nc);
+  RankingParams rp{rparams[0], rparams[1], rparams[2], rparams[3], 3, 13, ft_metric};
+  for (uint32_t i = 0; i < ncfg; ++i) {
+    std::vector<uint32_t> cfg(configs + (size_t)i * n, configs + (size_t)(i + 1) * n);
+    ProtocolStats st;
+    compute_stats(b, cfg, cl, st);
+    double score;
+    out_valid[i] = compute_score(n, st, rp, score) ? 1 : 0;
+    out_score[i] = score;
+  }
+  ORACLE_CATCH
+}
+
 void oracle_colex_unrank(uint64_t rank, uint32_t n, uint32_t ns, uint32_t* out) {
   Binom B(ns, n);
   colex_unrank(B, rank, n, ns, out);

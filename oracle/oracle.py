@@ -63,6 +63,8 @@ def lib():
         L.oracle_quorum_size.argtypes = [C.c_int, C.c_uint32, C.c_uint32]
         L.oracle_compute_stats.argtypes = [C.c_void_p, u32p, C.c_uint32, C.c_uint32, u32p, C.c_uint32,
                                            u64p, u32p]
+        L.oracle_scores.argtypes = [C.c_void_p, u32p, C.c_uint32, C.c_uint32, u32p, C.c_uint32, f64p, C.c_int,
+                                    f64p, np.ctypeslib.ndpointer(np.uint8, flags="C_CONTIGUOUS")]
         L.oracle_colex_unrank.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32, u32p]
         L.oracle_sweep.argtypes = [C.c_void_p, u32p, C.c_uint32, u32p, C.c_uint32, C.c_uint32,
                                    C.c_uint64, C.c_uint64, u32p, C.c_uint32, C.c_uint32, f64p, C.c_int,
@@ -144,6 +146,17 @@ class OraclePlanet:
         _check(lib().oracle_compute_stats(self.h, cfg.reshape(-1), ncfg, n, c, len(c),
                                           vals.reshape(-1), lead))
         return vals, lead
+
+    def scores(self, configs: np.ndarray, clients, rparams, ft_metric: int = 2):
+        """compute_score per config: (score f64, valid u8)."""
+        cfg = _u32(configs)
+        ncfg, n = cfg.shape
+        c = _u32(clients)
+        sc = np.zeros(ncfg, np.float64)
+        va = np.zeros(ncfg, np.uint8)
+        _check(lib().oracle_scores(self.h, cfg.reshape(-1), ncfg, n, c, len(c),
+                                   np.asarray(rparams, dtype=np.float64), ft_metric, sc, va))
+        return sc, va
 
     def sweep(self, servers, clients, n: int, rb: int, re: int, objectives, K: int,
               rparams=(110.0, 35.0, 0.0, 15.0), ft_metric: int = 2, threads: int = 1):

@@ -1,0 +1,338 @@
+"""GPU parity: the HIP path (libbote_hip.so through the C ABI) against the CPU
+oracle (oracle/) and the reference's own golden values.  Bit-exact for
+latencies, histograms, leaders, means, scores, validity and top-K identities;
+COV outputs within 1e-12 relative (the tolerance north_star allows is 1e-9).
+"""
+import json
+import math
+import os
+
+import numpy as np
+import pytest
+
+import oracle as O
+from fantoch_amd import _lib
+from fantoch_amd.bote import (DEFAULT_OBJECTIVES, DEFAULT_RANKING, Bote, DevicePlanet, FTMetric, RankingParams,
+                              Search, SearchInput, Sweep, eval_configs)
+from fantoch_amd.metrics import Stats
+from fantoch_amd.planet import AWS_2021_DIR, Planet, Region
+
+pytestmark = pytest.mark.gpu
+GOLD = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "reference_goldens.json")))
+COV_RTOL = 1e-12
+
+
+@pytest.fixture(scope="module")
+def gcp():
+    p = Planet.new()
+    return p, DevicePlanet(p), O.OraclePlanet.of(p)
+
+
+@pytest.fixture(scope="module")
+def bote():
+    return Bote.new()
+
+
+# ------------------------------------------------ lib.rs known answers ----
+def test_quorum_latencies(bote):
+    g = GOLD["quorum_latencies"]
+    for q, key in ((2, "q2"), (3, "q3")):
+        assert [bote.quorum_latency(r, g["regions"], q) for r in g["regions"]] == g[key]
+
+
+def test_leaderless(bote):
+    g = GOLD["leaderless"]
+    from fantoch_amd.metrics import Histogram
+    for case in g["cases"]:
+        h = Histogram.from_values(v for _, v in bote.leaderless(g["servers"], case["clients"], case["q"]))
+        assert (h.mean().round(), h.cov().round(), h.mdtm().round()) == (case["mean"], case["cov"], case["mdtm"])
+
+
+def test_leader(bote):
+    g = GOLD["leader"]
+    from fantoch_amd.metrics import Histogram
+    for case in g["cases"]:
+        h = Histogram.from_values(v for _, v in bote.leader(case["leader"], g["servers"], case["clients"], g["q"]))
+        assert (h.mean().round(), h.cov().round(), h.mdtm().round()) == (case["mean"], case["cov"], case["mdtm"])
+        stats = dict((r.name, hh) for r, hh in bote.all_leaders_stats(g["servers"], case["clients"], g["q"]))
+        assert stats[case["leader"]] == h
+
+
+def test_best_latency_leader(bote):
+    g = GOLD["best_latency_leader"]
+    _, h = bote.best_leader(g["servers"], g["servers"], g["q"], Stats.Mean)
+    assert (h.mean().round(), h.cov().round(), h.mdtm().round()) == (g["mean"], g["cov"], g["mdtm"])
+
+
+def test_single_config_api_vs_oracle(gcp):
+    p, dp, o = gcp
+    b = Bote(p)
+    rng = np.random.default_rng(7)
+    for _ in range(40):
+        ns = int(rng.integers(2, 12))
+        servers = rng.choice(p.R, ns, replace=False)
+        clients = rng.choice(p.R, int(rng.integers(1, 20)), replace=True)
+        q = int(rng.integers(1, ns + 1))
+        sv = [p.names[i] for i in servers]
+        cv = [p.names[i] for i in clients]
+        assert [v for _, v in b.leaderless(sv, cv, q)] == o.leaderless(servers, clients, q).tolist()
+        lead = int(rng.integers(0, p.R))
+        assert [v for _, v in b.leader(p.names[lead], sv, cv, q)] == o.leader(lead, servers, clients, q).tolist()
+        for stat in (Stats.Mean, Stats.COV, Stats.MDTM):
+            r, _ = b.best_leader(sv, cv, q, stat)
+            assert servers[o.best_leader(servers, clients, q, stat.value)] == p.idx(r)
+
+
+# ------------------------------------------------ compute_stats parity ----
+def _oracle_batch(o, srv, cli, cfg_pos):
+    regs = srv[cfg_pos]
+    return o.compute_stats(regs, cli)
+
+
+def _check_eval(o, dp, srv, cli, n, cfg_pos, ranking=None):
+    r = eval_configs(dp, srv, cli, n, configs=cfg_pos, ranking=ranking)
+    ov, ol = _oracle_batch(o, srv, cli, cfg_pos)
+    assert np.array_equal(r.vals.astype(np.uint64), np.where(ov == np.uint64(0xFFFFFFFFFFFFFFFF),
+                                                                np.uint64(0xFFFFFFFF), ov))
+    assert np.array_equal(r.leader, ol)
+    # moments and means against the oracle histograms
+    nc = len(cli)
+    for i in range(0, len(cfg_pos), max(1, len(cfg_pos) // 64)):
+        for slot in range(10):
+            vals = r.slot_values(i, slot)
+            if vals.size and vals[0] == 0xFFFFFFFF:
+                continue
+            st = O.hist_stats(vals)
+            assert r.mean[i, slot] == st[0]
+            if math.isnan(st[2]):
+                assert math.isnan(r.cov[i, slot])
+            else:
+                assert abs(r.cov[i, slot] - st[2]) <= COV_RTOL * abs(st[2])
+    return r
+
+
+def test_gcp_r20c20_n3_n5_all_configs(gcp):
+    """BASELINE config 1: GCP R=20, n=3,5, clients = all 20 — every config bit-exact."""
+    p, dp, o = gcp
+    srv = np.arange(p.R, dtype=np.uint32)
+    for n in (3, 5):
+        total = _lib.binomial(p.R, n)
+        cfg = np.array([_lib.colex_unrank(r, n, p.R) for r in range(total)], dtype=np.uint32)
+        _check_eval(o, dp, srv, srv, n, cfg)
+
+
+def test_gcp_all_n_sampled(gcp):
+    """BASELINE config 2: GCP n=2..13 (odd = reference, even = extension), sampled."""
+    p, dp, o = gcp
+    srv = np.arange(p.R, dtype=np.uint32)
+    rng = np.random.default_rng(11)
+    for n in range(2, 14):
+        total = _lib.binomial(p.R, n)
+        ranks = rng.choice(total, min(total, 1500), replace=False)
+        cfg = np.array([_lib.colex_unrank(int(r), n, p.R) for r in ranks], dtype=np.uint32)
+        _check_eval(o, dp, srv, srv, n, cfg)
+
+
+def test_rank_mode_equals_explicit(gcp):
+    p, dp, o = gcp
+    srv = np.arange(p.R, dtype=np.uint32)
+    n, rb, cnt = 7, 1234, 3000
+    a = eval_configs(dp, srv, srv, n, rank_begin=rb, ncfg=cnt)
+    cfg = np.array([_lib.colex_unrank(r, n, p.R) for r in range(rb, rb + cnt)], dtype=np.uint32)
+    b = eval_configs(dp, srv, srv, n, configs=cfg)
+    assert np.array_equal(a.vals, b.vals) and np.array_equal(a.leader, b.leader)
+
+
+def test_unsorted_servers_and_members(gcp):
+    """R13C13's server list is not in name order; members given out of order."""
+    p, dp, o = gcp
+    srv = p.idxs(GOLD["search"]["regions13"])
+    rng = np.random.default_rng(5)
+    for n in (3, 5, 6, 9):
+        cfg = np.array([rng.permutation(len(srv))[:n] for _ in range(300)], dtype=np.uint32)
+        _check_eval(o, dp, srv, srv, n, cfg)
+
+
+def test_client_subsets_and_single_client(gcp):
+    p, dp, o = gcp
+    srv = np.arange(p.R, dtype=np.uint32)
+    rng = np.random.default_rng(3)
+    for nc in (1, 2, 7, 33):
+        cli = rng.choice(p.R, nc, replace=nc > p.R).astype(np.uint32)
+        cfg = np.array([rng.permutation(p.R)[:5] for _ in range(200)], dtype=np.uint32)
+        _check_eval(o, dp, srv, cli, 5, cfg)
+
+
+def test_aws_2021_all_leaders():
+    """BASELINE config 3: AWS 2021_02_13 (R=5), FPaxos leader enumeration for every config."""
+    p = Planet.from_dir(AWS_2021_DIR)
+    dp = DevicePlanet(p)
+    o = O.OraclePlanet.of(p)
+    b = Bote(p)
+    srv = np.arange(p.R, dtype=np.uint32)
+    for n in (2, 3, 4, 5):
+        cfg = np.array([_lib.colex_unrank(r, n, p.R) for r in range(_lib.binomial(p.R, n))], dtype=np.uint32)
+        _check_eval(o, dp, srv, srv, n, cfg)
+        for c in cfg:
+            regs = [p.names[i] for i in c]
+            for q in (2, 3):
+                if q > n:
+                    continue
+                allst = b.all_leaders_stats(regs, p.names, q)
+                for (lr, h), l in zip(allst, c):
+                    assert list(h.iter_values()) == sorted(o.leader(int(l), c, srv, q).tolist())
+
+
+def test_score_and_validity_vs_oracle(gcp):
+    """Search::compute_score per config: bit-exact score and validity."""
+    p, dp, o = gcp
+    srv = np.arange(p.R, dtype=np.uint32)
+    for params in ((30, 10, 0, 15), (110, 35, 0, 15), (0, 0, -1, 0), (20, 5, 1, 0)):
+        rp = RankingParams.new(*params, 3, 13, FTMetric.F1F2)
+        for n in (3, 5, 11, 13):
+            total = _lib.binomial(p.R, n)
+            ranks = np.random.default_rng(n).choice(total, min(total, 3000), replace=False)
+            cfg = np.array([_lib.colex_unrank(int(x), n, p.R) for x in ranks], dtype=np.uint32)
+            g = eval_configs(dp, srv, srv, n, configs=cfg, ranking=rp, values=False)
+            sc, va = o.scores(srv[cfg], srv, [float(x) for x in params], 2)
+            assert np.array_equal(g.valid.astype(bool), va.astype(bool))
+            assert np.array_equal(g.score.view(np.uint64), sc.view(np.uint64))
+
+
+# ---------------------------------------------------- Search end-to-end ---
+def test_search_r13c13_golden():
+    """search.rs:671-751 through the GPU path."""
+    g = GOLD["search"]
+    search = Search(3, 13, SearchInput.R13C13)
+    params = RankingParams.new(110, 35, 0, 15, 3, 13, FTMetric.F1F2)
+    score, css, _clients = search.sorted_evolving_configs(params)[0]
+    assert score.round() == g["score"]
+    sorted_config = []
+    for cs in css:
+        for region in cs.config:
+            if region not in sorted_config:
+                sorted_config.append(region)
+        if len(cs.config) == 5:
+            assert Search.stats_fmt(cs.stats, 5) == g["stats_fmt_n5"]
+    assert [r.name for r in sorted_config] == g["sorted_config"]
+
+
+# ---------------------------------------------------- sweep and top-K -----
+def _oracle_sweep(o, srv, cli, n, rb, re, objectives, K, ranking, threads=16):
+    rp = (ranking.min_mean_fpaxos_improv, ranking.min_mean_epaxos_improv, ranking.min_fairness_fpaxos_improv,
+          ranking.min_mean_decrease)
+    return o.sweep(srv, cli, n, rb, re, objectives, K, rp, ranking.ft_metric.value, threads)
+
+
+@pytest.mark.parametrize("n,rb,re", [(3, 0, 1140), (5, 0, 15504), (7, 1000, 61000), (13, 0, 77520)])
+def test_sweep_topk_gcp_vs_oracle(gcp, n, rb, re):
+    p, dp, o = gcp
+    srv = np.arange(p.R, dtype=np.uint32)
+    rp = RankingParams.new(30, 10, 0, 15, 3, 13, FTMetric.F1F2)
+    sw = Sweep(dp, srv, srv, n, DEFAULT_OBJECTIVES, K=100, ranking=rp, digest=True)
+    sw.launch(rb, re)
+    got = sw.result()
+    tops, valid, digest = _oracle_sweep(o, srv, srv, n, rb, re, DEFAULT_OBJECTIVES, 100, rp)
+    assert got.valid == valid
+    assert got.digest == digest
+    for a, b in zip(got.tops, tops):
+        assert a == b
+
+
+def test_sweep_synthetic_r64_n7_subrange_vs_oracle():
+    """BASELINE config 4 workload on a bounded rank range, oracle-checked."""
+    p = Planet.synthetic(64)
+    dp = DevicePlanet(p)
+    o = O.OraclePlanet.of(p)
+    srv = np.arange(64, dtype=np.uint32)
+    total = _lib.binomial(64, 7)
+    for rb in (0, total // 2, total - 300_000):
+        re = rb + 300_000
+        sw = Sweep(dp, srv, srv, 7, DEFAULT_OBJECTIVES, K=100, ranking=DEFAULT_RANKING, digest=True)
+        sw.launch(rb, re)
+        got = sw.result()
+        tops, valid, digest = _oracle_sweep(o, srv, srv, 7, rb, re, DEFAULT_OBJECTIVES, 100, DEFAULT_RANKING)
+        assert (got.valid, got.digest) == (valid, digest)
+        assert got.tops == [list(t) for t in tops]
+
+
+def test_sweep_full_r64_n7_properties():
+    """Full 621,216,192-config sweep: shard invariance (merged top-K, valid
+    count and digest sum are independent of the split) and the reported top-K
+    keys re-derived by the oracle for those configs."""
+    p = Planet.synthetic(64)
+    dp = DevicePlanet(p)
+    o = O.OraclePlanet.of(p)
+    srv = np.arange(64, dtype=np.uint32)
+    sw = Sweep(dp, srv, srv, 7, DEFAULT_OBJECTIVES, K=100, ranking=DEFAULT_RANKING, digest=True)
+    total = sw.total
+    assert total == 621216192
+    sw.launch(0, total)
+    full = sw.result()
+    import torch
+    nb = sw.result_bytes()
+    blocks = torch.empty(3 * nb, dtype=torch.uint8, device="cuda")
+    cuts = [0, total // 3, 2 * total // 3, total]
+    for i in range(3):
+        sw.launch(cuts[i], cuts[i + 1])
+        sw.result_device(blocks.data_ptr() + i * nb)
+    out = torch.empty(nb, dtype=torch.uint8, device="cuda")
+    sw.merge_device(blocks.data_ptr(), 3, out.data_ptr())
+    torch.cuda.synchronize()
+    merged = sw.parse_block(out.cpu().numpy())
+    assert merged.tops == full.tops and merged.valid == full.valid and merged.digest == full.digest
+    # every reported record is re-derived by the oracle (keys bit-exact)
+    for oi, (kind, slot) in enumerate(DEFAULT_OBJECTIVES):
+        recs = full.tops[oi][:10]
+        for key, rank in recs:
+            tops, _, _ = _oracle_sweep(o, srv, srv, 7, rank, rank + 1, [(kind, slot)], 1, DEFAULT_RANKING, 1)
+            assert tops[0] == [(key, rank)]
+
+
+def test_near_tie_replay_equidistant():
+    """Equidistant planet: every FPaxos leader ties exactly -> device replay path."""
+    regions, p = Planet.equidistant(10, 9)
+    dp = DevicePlanet(p)
+    o = O.OraclePlanet.of(p)
+    srv = np.arange(p.R, dtype=np.uint32)
+    for n in (3, 4, 7):
+        cfg = np.array([_lib.colex_unrank(r, n, p.R) for r in range(_lib.binomial(p.R, n))], dtype=np.uint32)
+        _check_eval(o, dp, srv, srv, n, cfg)
+
+
+def test_zero_offdiagonal_planet():
+    """Off-diagonal zero latencies: the colocated nearest server is not the client itself."""
+    rng = np.random.default_rng(9)
+    R = 12
+    lat = rng.integers(0, 4, size=(R, R))
+    np.fill_diagonal(lat, 0)
+    p = Planet([f"z{i:02d}" for i in range(R)], lat)
+    dp = DevicePlanet(p)
+    o = O.OraclePlanet.of(p)
+    srv = np.arange(R, dtype=np.uint32)
+    for n in (2, 3, 5, 8, 12):
+        total = _lib.binomial(R, n)
+        cfg = np.array([_lib.colex_unrank(r, n, R) for r in range(min(total, 800))], dtype=np.uint32)
+        _check_eval(o, dp, srv, srv, n, cfg)
+
+
+def test_r128_n6_subrange_and_max_latency():
+    p = Planet.synthetic(128)
+    dp = DevicePlanet(p)
+    o = O.OraclePlanet.of(p)
+    srv = np.arange(128, dtype=np.uint32)
+    rb = _lib.binomial(128, 6) - 50_000
+    sw = Sweep(dp, srv, srv, 6, DEFAULT_OBJECTIVES, K=64, ranking=DEFAULT_RANKING, digest=True)
+    sw.launch(rb, rb + 50_000)
+    got = sw.result()
+    tops, valid, digest = _oracle_sweep(o, srv, srv, 6, rb, rb + 50_000, DEFAULT_OBJECTIVES, 64, DEFAULT_RANKING)
+    assert (got.valid, got.digest) == (valid, digest) and got.tops == [list(t) for t in tops]
+    # extreme latencies
+    lat = np.full((16, 16), 16383)
+    np.fill_diagonal(lat, 0)
+    lat[3, 5] = 1
+    q = Planet([f"m{i:02d}" for i in range(16)], lat)
+    qo = O.OraclePlanet.of(q)
+    s16 = np.arange(16, dtype=np.uint32)
+    cfg = np.array([_lib.colex_unrank(r, 9, 16) for r in range(0, _lib.binomial(16, 9), 7)], dtype=np.uint32)
+    _check_eval(qo, DevicePlanet(q), s16, s16, 9, cfg)
