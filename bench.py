@@ -110,7 +110,9 @@ def main():
     n = wl["n"]
     dp = DevicePlanet(planet, local)
     srv = np.arange(planet.R, dtype=np.uint32)
-    sweep = Sweep(dp, srv, srv, n, DEFAULT_OBJECTIVES, K=100, ranking=DEFAULT_RANKING, digest=False)
+    # digest=True: every config's 10 histogram moments and leader feed a
+    # checksum, so none of compute_stats' work can be skipped.
+    sweep = Sweep(dp, srv, srv, n, DEFAULT_OBJECTIVES, K=100, ranking=DEFAULT_RANKING, digest=True)
     total = sweep.total
     b, e = shard_range(total, world, rank)
     stream = torch.cuda.current_stream().cuda_stream
@@ -158,12 +160,14 @@ def main():
             "data": "synthetic" if wl["R"] else "gcp",
             "config": {"workload": wl["desc"], "regions": planet.R, "n": n, "configs_per_step": total,
                        "keys": 10, "objectives": len(DEFAULT_OBJECTIVES), "K": 100,
-                       "parallelism": f"rank-shard x{world}", "grid": grid, "block": block, "lds_bytes": lds},
+                       "parallelism": f"rank-shard x{world}", "grid": grid, "block": block, "lds_bytes": lds,
+                       "kernel_path": "fast" if sweep.is_fast() else "generic"},
             "roofline": {"bound": "valu", "achieved": achieved, "peak": VALU_PEAK_TOPS, "unit": "Tops/s",
                          "frac": achieved / VALU_PEAK_TOPS, "traffic": traffic,
                          "work_per_config": W, "kernel_ms_avg": kavg_ms,
                          "kernel": "eval_kernel<N,false> (bote_kernels.hip)"},
-            "result_check": {"valid": res.valid, "top_score_rank": res.tops[0][0][1] if res.tops[0] else None},
+            "result_check": {"valid": res.valid, "digest": res.digest,
+                             "top_score_rank": res.tops[0][0][1] if res.tops[0] else None},
         }
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(planet, n)

@@ -37,7 +37,7 @@ EXPORTS = [
     "bote_sweep_create", "bote_sweep_launch", "bote_sweep_result", "bote_sweep_result_bytes",
     "bote_sweep_result_device", "bote_merge_device", "bote_sweep_last_kernel_ms",
     "bote_sweep_destroy", "bote_colex_unrank", "bote_binomial", "bote_sweep_timing_reset",
-    "bote_sweep_timing", "bote_sweep_grid",
+    "bote_sweep_timing", "bote_sweep_grid", "bote_sweep_is_fast",
 ]
 
 
@@ -82,6 +82,14 @@ def lib():
     if not os.path.exists(LIB_PATH):
         raise ImportError(f"{LIB_PATH} is missing: build it with `make -C {CSRC}` "
                           "(there is no CPU fallback for the HIP path)")
+    # One HIP runtime per process: PyTorch ROCm bundles libamdhip64 (soname
+    # libamdhip64.so.7) and needs it under its unversioned name, so once
+    # /opt/rocm's copy is loaded first torch finds no device.  Loading torch
+    # first makes our DT_NEEDED libamdhip64.so.7 resolve to the same runtime.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = C.CDLL(LIB_PATH)
     L.bote_last_error.restype = C.c_char_p
     L.bote_device_count.argtypes = [C.POINTER(C.c_int)]
@@ -114,6 +122,7 @@ def lib():
     L.bote_sweep_timing_reset.argtypes = [_vp]
     L.bote_sweep_timing.argtypes = [_vp, C.POINTER(C.c_float), C.POINTER(C.c_uint32)]
     L.bote_sweep_grid.argtypes = [_vp, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
+    L.bote_sweep_is_fast.argtypes = [_vp, C.POINTER(C.c_int)]
     L.bote_colex_unrank.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32, _u32p]
     L.bote_binomial.restype = C.c_uint64
     L.bote_binomial.argtypes = [C.c_uint32, C.c_uint32]

@@ -512,6 +512,11 @@ class Sweep:
         check(lib().bote_sweep_timing(self.h, C.byref(ms), C.byref(n)))
         return ms.value, n.value
 
+    def is_fast(self) -> bool:
+        v = C.c_int()
+        check(lib().bote_sweep_is_fast(self.h, C.byref(v)))
+        return bool(v.value)
+
     def geometry(self) -> Tuple[int, int, int]:
         g, b, l = C.c_uint32(), C.c_uint32(), C.c_uint32()
         check(lib().bote_sweep_grid(self.h, C.byref(g), C.byref(b), C.byref(l)))

@@ -114,8 +114,48 @@ struct bote_sweep {
   std::vector<std::pair<hipEvent_t, hipEvent_t>> evpool;
   size_t ev_used = 0;
   bool launched = false;
+  // fast path (bote_sweep.hip) + exact fixup of its deferred configs
+  bool fast = false;
+  bote::FastArgs fargs{};
+  uint32_t fgrid = 0;
+  size_t fshm = 0;
+  uint32_t xgrid = 0;  // generic fixup grid (deferred configs)
+  DBuf cqt, rqt, queue, qcount;
+  uint64_t last_rb = 0, last_re = 0;
+  hipStream_t last_stream = nullptr;
   uint64_t result_bytes() const { return (uint64_t)n_obj * bote::KP * 16 + 16; }
 };
+
+namespace {
+constexpr uint64_t QUEUE_CAP = 1ull << 20;  // deferred near-tie configs per launch
+
+// The fast path's preconditions (bote_sweep.hip header).
+bool fast_eligible(const bote_planet* p, const uint32_t* servers, uint32_t ns, uint32_t nc,
+                   const bote_ranking_params* rp) {
+  if (nc < 2) return false;
+  if (!std::is_sorted(servers, servers + ns)) return false;
+  if (rp && rp->min_fairness_fpaxos_improv != 0.0) return false;
+  for (size_t i = 0; i < p->lat.size(); ++i)
+    if (p->lat[i] > 4095) return false;
+  for (uint32_t i = 0; i < ns; ++i)
+    for (uint32_t j = 0; j < ns; ++j) {
+      uint16_t v = p->lat[(size_t)servers[i] * p->R + servers[j]];
+      if (i == j ? v != 0 : v == 0) return false;
+    }
+  return true;
+}
+
+// Column-major packed-u16 quad layout: col t, quad g, lane i = row rows[4g+i].
+std::vector<uint16_t> quad_layout(const bote_planet* p, const uint32_t* rows, uint32_t nrows, uint32_t& quads) {
+  quads = (nrows + 3) / 4;
+  const uint32_t stride = (quads + 1) * 4;  // u16 per column (one pad slot)
+  std::vector<uint16_t> m((size_t)p->R * stride, 0);
+  for (uint32_t t = 0; t < p->R; ++t)
+    for (uint32_t c = 0; c < nrows; ++c)
+      m[(size_t)t * stride + c] = (uint16_t)(p->lat[(size_t)rows[c] * p->R + t] << bote::LAT_SHIFT);
+  return m;
+}
+}  // namespace
 
 extern "C" {
 
@@ -480,48 +520,91 @@ int bote_sweep_create(const bote_planet* p, const uint32_t* servers, uint32_t ns
   if (s->shm > device_max_lds(p->device)) return cleanup(fail(BOTE_E_RANGE, "planet/client set too large for LDS"));
   int nb = bote::eval_occupancy(n, false, s->bd, s->shm);
   s->grid = (uint32_t)(device_cus(p->device) * nb);
-  size_t top_bytes = (size_t)s->grid * std::max<uint32_t>(n_obj, 1) * bote::KP * 16;
-  size_t tmp_bytes = (size_t)((s->grid + 7) / 8) * std::max<uint32_t>(n_obj, 1) * bote::KP * 16;
+  s->xgrid = 32;
+
+  // ---- fast path: quad layouts, column sums are computed on the device
+  s->fast = fast_eligible(p, servers, ns, nc, has_score ? rp : nullptr) && !getenv("BOTE_FORCE_GENERIC");
+  if (s->fast) {
+    bote::FastArgs& f = s->fargs;
+    f = bote::FastArgs{};
+    std::vector<uint32_t> ident(p->R);
+    for (uint32_t i = 0; i < p->R; ++i) ident[i] = i;
+    bool cli_ident = nc == p->R && std::equal(clients, clients + nc, ident.begin());
+    uint32_t cq_quads = 0, rq_quads = 0;
+    auto cq = quad_layout(p, clients, nc, cq_quads);
+    std::vector<uint16_t> rq;
+    if (!cli_ident) rq = quad_layout(p, ident.data(), p->R, rq_quads);
+    if (s->cqt.alloc(cq.size() * 2) != hipSuccess || (!cli_ident && s->rqt.alloc(rq.size() * 2) != hipSuccess) ||
+        s->queue.alloc(QUEUE_CAP * 8) != hipSuccess || s->qcount.alloc(16) != hipSuccess)
+      return cleanup(fail(BOTE_E_NOMEM, "hipMalloc fast-path buffers"));
+    if (hipMemcpy(s->cqt.p, cq.data(), cq.size() * 2, hipMemcpyHostToDevice) != hipSuccess ||
+        (!cli_ident && hipMemcpy(s->rqt.p, rq.data(), rq.size() * 2, hipMemcpyHostToDevice) != hipSuccess))
+      return cleanup(fail(BOTE_E_DEVICE, "upload fast-path layouts"));
+    f.cqt = s->cqt.as<uint2>();
+    f.rqt = cli_ident ? s->cqt.as<uint2>() : s->rqt.as<uint2>();
+    f.rq_separate = cli_ident ? 0 : 1;
+    f.R = p->R;
+    f.cq_quads = cq_quads;
+    f.rq_quads = cli_ident ? cq_quads : rq_quads;
+    f.srv = s->srv.as<uint32_t>();
+    f.ns = ns;
+    f.srv_identity = 1;
+    for (uint32_t i = 0; i < ns; ++i) f.srv_identity &= servers[i] == i;
+    f.nc = nc;
+    f.binom = s->binom.as<uint64_t>();
+    uint32_t maxlat = 0;
+    for (auto v : p->lat) maxlat = std::max<uint32_t>(maxlat, v);
+    const uint64_t amax = 2ull * maxlat, per_quad = 4 * amax * amax;
+    f.s2_flush = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(1u << 20, per_quad ? 0xFFFFFFFFull / per_quad : 1u << 20));
+    f.want_score = a.want_score;
+    f.p_fmean = a.p_fmean;
+    f.p_emean = a.p_emean;
+    f.ft_metric = a.ft_metric;
+    auto integral = [](double x) { return x == (double)(int64_t)x && x > -1e12 && x < 1e12; };
+    f.p_int = integral(a.p_fmean) && integral(a.p_emean) ? 1 : 0;
+    f.n_obj = a.n_obj;
+    for (int o = 0; o < bote::MAXOBJ; ++o) {
+      f.obj_kind[o] = a.obj_kind[o];
+      f.obj_slot[o] = a.obj_slot[o];
+    }
+    f.K = K;
+    f.out_counters = a.out_counters;
+    f.want_digest = a.want_digest;
+    f.queue = s->queue.as<uint64_t>();
+    f.queue_count = s->qcount.as<unsigned long long>();
+    f.queue_cap = QUEUE_CAP;
+    s->fshm = bote::fast_smem_bytes(f, n);
+    if (s->fshm > device_max_lds(p->device)) {
+      s->fast = false;
+    } else {
+      s->fgrid = (uint32_t)(device_cus(p->device) * bote::fast_occupancy(n, s->fshm));
+    }
+  }
+  const uint32_t lists = s->fast ? s->fgrid + s->xgrid : s->grid;
+  size_t top_bytes = (size_t)lists * std::max<uint32_t>(n_obj, 1) * bote::KP * 16;
+  size_t tmp_bytes = (size_t)((lists + 7) / 8) * std::max<uint32_t>(n_obj, 1) * bote::KP * 16;
   if (s->top.alloc(top_bytes) != hipSuccess || s->tmp0.alloc(tmp_bytes) != hipSuccess ||
       s->tmp1.alloc(tmp_bytes) != hipSuccess || s->result.alloc(s->result_bytes()) != hipSuccess)
     return cleanup(fail(BOTE_E_NOMEM, "hipMalloc sweep workspace"));
   a.out_top = n_obj ? s->top.as<Rec>() : nullptr;
+  s->fargs.out_top = a.out_top;
   if (hipEventCreate(&s->ev0) != hipSuccess || hipEventCreate(&s->ev1) != hipSuccess)
     return cleanup(fail(BOTE_E_DEVICE, "hipEventCreate"));
   *out = s;
   return BOTE_OK;
 }
 
-int bote_sweep_launch(bote_sweep* s, uint64_t rank_begin, uint64_t rank_end, void* hip_stream) {
-  if (!s) return fail(BOTE_E_ARG, "sweep is null");
-  uint64_t total = binom_u64(s->ns, s->n);
-  if (rank_begin > rank_end || rank_end > total) return fail(BOTE_E_ARG, "rank range out of bounds");
-  HIP_TRY(hipSetDevice(s->p->device));
-  hipStream_t st = (hipStream_t)hip_stream;
-  EvalArgs a = s->args;
-  a.rb = rank_begin;
-  a.re = rank_end;
-  const uint64_t count = rank_end - rank_begin;
-  const uint64_t G = (uint64_t)s->grid * s->bd;
-  a.runlen = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(32, count / (G * 8)));
-  HIP_TRY(hipMemsetAsync(s->counters.p, 0, 16, st));
-  if (s->ev_used == s->evpool.size()) {
-    hipEvent_t e0, e1;
-    HIP_TRY(hipEventCreate(&e0));
-    HIP_TRY(hipEventCreate(&e1));
-    s->evpool.emplace_back(e0, e1);
-  }
-  auto& tp = s->evpool[s->ev_used++];
-  HIP_TRY(hipEventRecord(s->ev0, st));
-  HIP_TRY(hipEventRecord(tp.first, st));
-  HIP_TRY(bote::launch_eval(a, s->n, false, s->grid, s->bd, s->shm, st));
-  HIP_TRY(hipEventRecord(tp.second, st));
-  HIP_TRY(hipEventRecord(s->ev1, st));
-  // merge the per-block lists down to one: [o][KP] at the head of `result`
+int bote_sweep_is_fast(const bote_sweep* s, int* out) {
+  if (!s || !out) return fail(BOTE_E_ARG, "null argument");
+  *out = s->fast ? 1 : 0;
+  return BOTE_OK;
+}
+
+// Merge `lists` per-block lists into the result block and append the counters.
+static int merge_chain(bote_sweep* s, uint32_t lists, hipStream_t st) {
   const uint64_t lstride = (uint64_t)s->n_obj * bote::KP;
   Rec* rec_out = s->result.as<Rec>();
   if (s->n_obj) {
-    uint32_t lists = s->grid;
     const Rec* src = s->top.as<Rec>();
     Rec* bufs[2] = {s->tmp0.as<Rec>(), s->tmp1.as<Rec>()};
     int b = 0;
@@ -534,6 +617,98 @@ int bote_sweep_launch(bote_sweep* s, uint64_t rank_begin, uint64_t rank_end, voi
     HIP_TRY(bote::launch_merge(src, lists, lstride, rec_out, lstride, s->n_obj, st));
   }
   HIP_TRY(hipMemcpyAsync((char*)s->result.p + lstride * 16, s->counters.p, 16, hipMemcpyDeviceToDevice, st));
+  return BOTE_OK;
+}
+
+static int timing_slot(bote_sweep* s, hipEvent_t*& e0, hipEvent_t*& e1) {
+  if (s->ev_used == s->evpool.size()) {
+    hipEvent_t a0, a1;
+    HIP_TRY(hipEventCreate(&a0));
+    HIP_TRY(hipEventCreate(&a1));
+    s->evpool.emplace_back(a0, a1);
+  }
+  auto& tp = s->evpool[s->ev_used++];
+  e0 = &tp.first;
+  e1 = &tp.second;
+  return BOTE_OK;
+}
+
+// Generic kernel over [rb, re): the exact path for any planet.
+static int launch_generic(bote_sweep* s, uint64_t rb, uint64_t re, hipStream_t st, bool timed) {
+  EvalArgs a = s->args;
+  a.rb = rb;
+  a.re = re;
+  const uint64_t count = re - rb;
+  const uint64_t G = (uint64_t)s->grid * s->bd;
+  a.runlen = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(32, count / (G * 8)));
+  HIP_TRY(hipMemsetAsync(s->counters.p, 0, 16, st));
+  hipEvent_t *e0 = nullptr, *e1 = nullptr;
+  int rc;
+  if (timed && (rc = timing_slot(s, e0, e1))) return rc;
+  HIP_TRY(hipEventRecord(s->ev0, st));
+  if (e0) HIP_TRY(hipEventRecord(*e0, st));
+  HIP_TRY(bote::launch_eval(a, s->n, false, s->grid, s->bd, s->shm, st));
+  if (e1) HIP_TRY(hipEventRecord(*e1, st));
+  HIP_TRY(hipEventRecord(s->ev1, st));
+  return merge_chain(s, s->grid, st);
+}
+
+// Fast kernel over [rb, re), then the generic kernel over its deferred ranks.
+static int launch_fast_path(bote_sweep* s, uint64_t rb, uint64_t re, hipStream_t st) {
+  bote::FastArgs f = s->fargs;
+  f.rb = rb;
+  f.re = re;
+  const uint64_t count = re - rb;
+  const uint64_t G = (uint64_t)s->fgrid * bote::FAST_BD;
+  f.runlen = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(32, count / (G * 8)));
+  HIP_TRY(hipMemsetAsync(s->counters.p, 0, 16, st));
+  HIP_TRY(hipMemsetAsync(s->qcount.p, 0, 8, st));
+  hipEvent_t *e0 = nullptr, *e1 = nullptr;
+  int rc;
+  if ((rc = timing_slot(s, e0, e1))) return rc;
+  HIP_TRY(hipEventRecord(s->ev0, st));
+  HIP_TRY(hipEventRecord(*e0, st));
+  HIP_TRY(bote::launch_fast(f, s->n, s->fgrid, s->fshm, st));
+  HIP_TRY(hipEventRecord(*e1, st));
+  HIP_TRY(hipEventRecord(s->ev1, st));
+  // exact fixup of the deferred configs: generic kernel over the rank list
+  EvalArgs a = s->args;
+  a.rank_list = s->queue.as<uint64_t>();
+  a.rank_count = s->qcount.as<unsigned long long>();
+  a.rb = 0;
+  a.re = QUEUE_CAP;
+  a.runlen = 1;
+  a.out_top = s->n_obj ? s->top.as<Rec>() + (size_t)s->fgrid * s->n_obj * bote::KP : nullptr;
+  HIP_TRY(bote::launch_eval(a, s->n, false, s->xgrid, s->bd, s->shm, st));
+  return merge_chain(s, s->fgrid + s->xgrid, st);
+}
+
+// After a fast-path launch: if more configs were deferred than the queue
+// holds, recompute the whole range on the generic path (synchronous).
+static int ensure_complete(bote_sweep* s, hipStream_t st) {
+  if (!s->fast) return BOTE_OK;
+  unsigned long long q = 0;
+  HIP_TRY(hipMemcpyAsync(&q, s->qcount.p, 8, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  if (q <= QUEUE_CAP) return BOTE_OK;
+  int rc = launch_generic(s, s->last_rb, s->last_re, st, false);
+  if (rc) return rc;
+  HIP_TRY(hipMemsetAsync(s->qcount.p, 0, 8, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  return BOTE_OK;
+}
+
+int bote_sweep_launch(bote_sweep* s, uint64_t rank_begin, uint64_t rank_end, void* hip_stream) {
+  if (!s) return fail(BOTE_E_ARG, "sweep is null");
+  uint64_t total = binom_u64(s->ns, s->n);
+  if (rank_begin > rank_end || rank_end > total) return fail(BOTE_E_ARG, "rank range out of bounds");
+  HIP_TRY(hipSetDevice(s->p->device));
+  hipStream_t st = (hipStream_t)hip_stream;
+  int rc = s->fast ? launch_fast_path(s, rank_begin, rank_end, st) : launch_generic(s, rank_begin, rank_end, st, true);
+  if (rc) return rc;
+  s->last_rb = rank_begin;
+  s->last_re = rank_end;
+  s->last_stream = st;
   s->launched = true;
   return BOTE_OK;
 }
@@ -544,6 +719,8 @@ int bote_sweep_result_device(bote_sweep* s, void* dst, void* hip_stream) {
   if (!s || !dst) return fail(BOTE_E_ARG, "null argument");
   if (!s->launched) return fail(BOTE_E_ARG, "sweep not launched");
   HIP_TRY(hipSetDevice(s->p->device));
+  int rc = ensure_complete(s, (hipStream_t)hip_stream);
+  if (rc) return rc;
   HIP_TRY(hipMemcpyAsync(dst, s->result.p, s->result_bytes(), hipMemcpyDeviceToDevice, (hipStream_t)hip_stream));
   return BOTE_OK;
 }
@@ -572,6 +749,8 @@ int bote_sweep_result(bote_sweep* s, void* hip_stream, bote_topk_record* out, ui
   if (!s) return fail(BOTE_E_ARG, "sweep is null");
   if (!s->launched) return fail(BOTE_E_ARG, "sweep not launched");
   HIP_TRY(hipSetDevice(s->p->device));
+  int rc = ensure_complete(s, (hipStream_t)hip_stream);
+  if (rc) return rc;
   std::vector<uint8_t> blk(s->result_bytes());
   HIP_TRY(hipMemcpyAsync(blk.data(), s->result.p, blk.size(), hipMemcpyDeviceToHost, (hipStream_t)hip_stream));
   HIP_TRY(hipStreamSynchronize((hipStream_t)hip_stream));
@@ -623,9 +802,9 @@ int bote_sweep_timing(bote_sweep* s, float* out_total_ms, uint32_t* out_launches
 
 int bote_sweep_grid(const bote_sweep* s, uint32_t* out_grid, uint32_t* out_block, uint32_t* out_lds_bytes) {
   if (!s) return fail(BOTE_E_ARG, "sweep is null");
-  if (out_grid) *out_grid = s->grid;
-  if (out_block) *out_block = s->bd;
-  if (out_lds_bytes) *out_lds_bytes = (uint32_t)s->shm;
+  if (out_grid) *out_grid = s->fast ? s->fgrid : s->grid;
+  if (out_block) *out_block = s->fast ? bote::FAST_BD : s->bd;
+  if (out_lds_bytes) *out_lds_bytes = (uint32_t)(s->fast ? s->fshm : s->shm);
   return BOTE_OK;
 }
 

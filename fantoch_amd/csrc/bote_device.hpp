@@ -225,6 +225,27 @@ __device__ __forceinline__ bool rec_lt(const Rec& a, const Rec& b) {
 }
 __device__ __forceinline__ Rec rec_max() { return Rec{~0ull, ~0ull}; }
 
+// COV objective key (BOTE_OBJ_COV): bits of fl64(V / S1^2); all-ones when the
+// reference's COV is NaN.  Monotone in the true COV.
+__device__ __forceinline__ uint64_t cov_key(const Mom& m) {
+  if (cov_nan(m)) return ~0ull;
+  double rr = (double)mom_v(m) / ((double)m.s1 * (double)m.s1);
+  return (uint64_t)__double_as_longlong(rr);
+}
+
+// Per-config digest (DESIGN.md "Digest"), summed over configs mod 2^64:
+//   h = 0; for each present slot s ascending:
+//     h = (h ^ lo32(s1_s)) * 0x9E3779B1;  h = (h ^ lo32(s2_s ^ (s2_s >> 32))) * 0x85EBCA77
+//   d = mix64(rank ^ (leader_pos << 56) ^ (h << 24))
+__device__ __forceinline__ uint32_t digest_fold(uint32_t h, uint64_t s1, uint64_t s2) {
+  h = (h ^ (uint32_t)s1) * 0x9E3779B1u;
+  h = (h ^ (uint32_t)(s2 ^ (s2 >> 32))) * 0x85EBCA77u;
+  return h;
+}
+__device__ __forceinline__ uint64_t digest_final(uint64_t rank, uint32_t lead, uint32_t h) {
+  return mix64(rank ^ ((uint64_t)lead << 56) ^ ((uint64_t)h << 24));
+}
+
 // In-LDS bitonic sort of a[0..n), n a power of two, by the whole block.
 __device__ inline void block_bitonic(Rec* a, int n) {
   for (int k = 2; k <= n; k <<= 1) {
@@ -243,6 +264,131 @@ __device__ inline void block_bitonic(Rec* a, int n) {
       __syncthreads();
     }
   }
+}
+
+}  // namespace bote
+
+namespace bote {
+
+// ----------------------------------------------- block-level top-K in LDS --
+// Each objective keeps a sorted list of KP records; `thr[o]` is its K-th
+// record.  A config enters the candidate buffer only if it beats thr[o]; the
+// block merges candidates one objective at a time (bitonic sort + merge path).
+struct TopkLds {
+  Rec* top;   // MAXOBJ * KP
+  Rec* cand;  // blockDim.x
+  Rec* tmp;   // KP
+  Rec* thr;   // MAXOBJ
+  int* cnt;
+};
+
+__device__ inline int lower_bound_rec(const Rec* a, int n, const Rec& x) {
+  int lo = 0, hi = n;
+  while (lo < hi) {
+    int mid = (lo + hi) >> 1;
+    if (rec_lt(a[mid], x)) lo = mid + 1; else hi = mid;
+  }
+  return lo;
+}
+__device__ inline int upper_bound_rec(const Rec* a, int n, const Rec& x) {
+  int lo = 0, hi = n;
+  while (lo < hi) {
+    int mid = (lo + hi) >> 1;
+    if (!rec_lt(x, a[mid])) lo = mid + 1; else hi = mid;
+  }
+  return lo;
+}
+
+__device__ inline void topk_init(const TopkLds& t, int n_obj) {
+  for (uint32_t i = threadIdx.x; i < (uint32_t)n_obj * KP; i += blockDim.x) t.top[i] = rec_max();
+  if (threadIdx.x < MAXOBJ) t.thr[threadIdx.x] = rec_max();
+  if (threadIdx.x == 0) *t.cnt = 0;
+}
+
+// Merge the candidate buffer (*t.cnt entries) into objective o's list.
+__device__ inline void topk_merge(const TopkLds& t, int o, uint32_t K) {
+  const int BD = blockDim.x, tid = threadIdx.x;
+  const int n = *t.cnt;
+  if (tid >= n) t.cand[tid] = rec_max();
+  __syncthreads();
+  block_bitonic(t.cand, BD);
+  Rec* top = t.top + o * KP;
+  if (tid < KP) {
+    Rec x = top[tid];
+    int r = tid + lower_bound_rec(t.cand, BD, x);
+    if (r < KP) t.tmp[r] = x;
+  }
+  {
+    Rec y = t.cand[tid];
+    int r = tid + upper_bound_rec(top, KP, y);
+    if (r < KP) t.tmp[r] = y;
+  }
+  __syncthreads();
+  if (tid < KP) top[tid] = t.tmp[tid];
+  __syncthreads();
+  if (tid == 0) {
+    t.thr[o] = top[K - 1];
+    *t.cnt = 0;
+  }
+  __syncthreads();
+}
+
+// One block-synchronous step: every thread of the block must call it.
+// ok[o] false = this lane offers nothing for objective o.
+__device__ __forceinline__ void topk_step(const TopkLds& t, int n_obj, uint32_t K, const uint64_t (&key)[MAXOBJ],
+                                          const bool (&ok)[MAXOBJ], uint64_t rank) {
+  bool pass[MAXOBJ];
+  bool any = false;
+#pragma unroll
+  for (int o = 0; o < MAXOBJ; ++o) {
+    pass[o] = o < n_obj && ok[o] && rec_lt(Rec{key[o], rank}, t.thr[o]);
+    any = any || pass[o];
+  }
+  if (__syncthreads_or(any)) {
+#pragma unroll
+    for (int o = 0; o < MAXOBJ; ++o) {
+      if (o >= n_obj) break;
+      if (pass[o] && rec_lt(Rec{key[o], rank}, t.thr[o])) {
+        int i = atomicAdd(t.cnt, 1);
+        t.cand[i] = Rec{key[o], rank};
+      }
+      __syncthreads();
+      if (*t.cnt > 0) topk_merge(t, o, K);
+    }
+  }
+}
+
+// ----------------------------------------------------- colex enumeration --
+// rank = sum_j C(p_j, j+1) with p ascending (an extension: the reference's
+// permutator order is not pinned).
+template <int N>
+__device__ __forceinline__ void colex_unrank(const uint64_t* binom, uint32_t ns, uint64_t rank, uint32_t (&p)[N]) {
+  uint64_t r = rank;
+  uint32_t hi = ns;
+#pragma unroll
+  for (int j = N - 1; j >= 0; --j) {
+    const uint32_t k = j + 1;
+    uint32_t lo = j, up = hi;  // answer in [lo, up)
+    while (up - lo > 1) {
+      uint32_t mid = (lo + up) >> 1;
+      if (binom[mid * (N + 1) + k] <= r) lo = mid; else up = mid;
+    }
+    p[j] = lo;
+    r -= binom[lo * (N + 1) + k];
+    hi = lo;
+  }
+}
+
+template <int N>
+__device__ __forceinline__ void colex_next(uint32_t ns, uint32_t (&p)[N]) {
+  uint32_t js = N;  // first j with p[j] + 1 < p[j+1]
+#pragma unroll
+  for (int j = N - 1; j >= 0; --j) {
+    uint32_t nxt = (j == N - 1) ? ns : p[j + 1];
+    if (p[j] + 1 < nxt) js = j;
+  }
+#pragma unroll
+  for (int j = 0; j < N; ++j) p[j] = (uint32_t)j < js ? (uint32_t)j : ((uint32_t)j == js ? p[j] + 1 : p[j]);
 }
 
 }  // namespace bote

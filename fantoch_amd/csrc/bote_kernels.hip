@@ -29,11 +29,7 @@ struct Smem {
   uint64_t* cs;      // 2*ns  per position: sum_c L[c][srv[p]], sum_c L^2
   uint64_t* binom;   // (ns+1)*(N+1)
   uint32_t* qtab;    // N * BD * NLW
-  Rec* top;          // MAXOBJ * KP
-  Rec* cand;         // BD
-  Rec* tmp;          // KP
-  Rec* thr;          // MAXOBJ
-  int* cnt;
+  TopkLds tk;        // top MAXOBJ*KP, cand BD, tmp KP, thr MAXOBJ, cnt
 };
 
 __host__ __device__ inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
@@ -70,11 +66,11 @@ __device__ inline Smem carve(const EvalArgs& a, unsigned char* base, int NLW) {
   s.cs = (uint64_t*)(base + off[3]);
   s.binom = (uint64_t*)(base + off[4]);
   s.qtab = (uint32_t*)(base + off[5]);
-  s.top = (Rec*)(base + off[6]);
-  s.cand = (Rec*)(base + off[7]);
-  s.tmp = (Rec*)(base + off[8]);
-  s.thr = (Rec*)(base + off[9]);
-  s.cnt = (int*)(base + off[10]);
+  s.tk.top = (Rec*)(base + off[6]);
+  s.tk.cand = (Rec*)(base + off[7]);
+  s.tk.tmp = (Rec*)(base + off[8]);
+  s.tk.thr = (Rec*)(base + off[9]);
+  s.tk.cnt = (int*)(base + off[10]);
   return s;
 }
 
@@ -86,39 +82,6 @@ __device__ __forceinline__ uint32_t sel(const uint32_t (&arr)[N], uint32_t i) {
 #pragma unroll
   for (int j = 0; j < N; ++j) r |= arr[j] & (0u - (uint32_t)(i == (uint32_t)j));
   return r;
-}
-
-// ----------------------------------------------------- colex enumeration --
-// rank = sum_j C(p_j, j+1) with p ascending (an extension: the reference's
-// permutator order is not pinned).
-template <int N>
-__device__ __forceinline__ void colex_unrank(const uint64_t* binom, uint32_t ns, uint64_t rank, uint32_t (&p)[N]) {
-  uint64_t r = rank;
-  uint32_t hi = ns;
-#pragma unroll
-  for (int j = N - 1; j >= 0; --j) {
-    const uint32_t k = j + 1;
-    uint32_t lo = j, up = hi;  // answer in [lo, up)
-    while (up - lo > 1) {
-      uint32_t mid = (lo + up) >> 1;
-      if (binom[mid * (N + 1) + k] <= r) lo = mid; else up = mid;
-    }
-    p[j] = lo;
-    r -= binom[lo * (N + 1) + k];
-    hi = lo;
-  }
-}
-
-template <int N>
-__device__ __forceinline__ void colex_next(uint32_t ns, uint32_t (&p)[N]) {
-  uint32_t js = N;  // first j with p[j] + 1 < p[j+1]
-#pragma unroll
-  for (int j = N - 1; j >= 0; --j) {
-    uint32_t nxt = (j == N - 1) ? ns : p[j + 1];
-    if (p[j] + 1 < nxt) js = j;
-  }
-#pragma unroll
-  for (int j = 0; j < N; ++j) p[j] = (uint32_t)j < js ? (uint32_t)j : ((uint32_t)j == js ? p[j] + 1 : p[j]);
 }
 
 // --------------------------------------------------------- config result --
@@ -401,52 +364,6 @@ __device__ __forceinline__ void eval_config(const EvalArgs& a, const Smem& s, co
   }
 }
 
-// ----------------------------------------------------- block top-K (LDS) --
-__device__ inline int lower_bound_rec(const Rec* a, int n, const Rec& x) {
-  int lo = 0, hi = n;
-  while (lo < hi) {
-    int mid = (lo + hi) >> 1;
-    if (rec_lt(a[mid], x)) lo = mid + 1; else hi = mid;
-  }
-  return lo;
-}
-__device__ inline int upper_bound_rec(const Rec* a, int n, const Rec& x) {
-  int lo = 0, hi = n;
-  while (lo < hi) {
-    int mid = (lo + hi) >> 1;
-    if (!rec_lt(x, a[mid])) lo = mid + 1; else hi = mid;
-  }
-  return lo;
-}
-
-// Merge the block's candidate buffer (s.cnt entries) into objective o's list.
-__device__ void topk_merge(const Smem& s, int o, uint32_t K) {
-  const int BD = blockDim.x, tid = threadIdx.x;
-  const int n = *s.cnt;
-  if (tid >= n) s.cand[tid] = rec_max();
-  __syncthreads();
-  block_bitonic(s.cand, BD);
-  Rec* top = s.top + o * KP;
-  if (tid < KP) {
-    Rec x = top[tid];
-    int r = tid + lower_bound_rec(s.cand, BD, x);
-    if (r < KP) s.tmp[r] = x;
-  }
-  {
-    Rec y = s.cand[tid];
-    int r = tid + upper_bound_rec(top, KP, y);
-    if (r < KP) s.tmp[r] = y;
-  }
-  __syncthreads();
-  if (tid < KP) top[tid] = s.tmp[tid];
-  __syncthreads();
-  if (tid == 0) {
-    s.thr[o] = top[K - 1];
-    *s.cnt = 0;
-  }
-  __syncthreads();
-}
-
 // ------------------------------------------------------------ the kernel --
 template <int N, bool FULL>
 __global__ void __launch_bounds__(256) eval_kernel(EvalArgs a) {
@@ -463,11 +380,7 @@ __global__ void __launch_bounds__(256) eval_kernel(EvalArgs a) {
   for (uint32_t i = tid; i < a.ns; i += BD) s.srv[i] = a.srv[i];
   if (!a.cfgs)
     for (uint32_t i = tid; i < (a.ns + 1) * (N + 1); i += BD) s.binom[i] = a.binom[i];
-  if (topk) {
-    for (uint32_t i = tid; i < MAXOBJ * KP; i += BD) s.top[i] = rec_max();
-    if (tid < MAXOBJ) s.thr[tid] = rec_max();
-    if (tid == 0) *s.cnt = 0;
-  }
+  if (topk) topk_init(s.tk, a.n_obj);
   __syncthreads();
   for (uint32_t i = tid; i < a.ns; i += BD) {
     uint64_t c1 = 0, c2 = 0;
@@ -482,8 +395,12 @@ __global__ void __launch_bounds__(256) eval_kernel(EvalArgs a) {
   }
   __syncthreads();
 
-  const uint64_t total = a.re - a.rb;
-  const uint64_t runlen = a.runlen;
+  uint64_t total = a.re - a.rb;
+  if (a.rank_list) {  // deferred configs: the count is known only on the device
+    const uint64_t c = *a.rank_count;
+    total = c < total ? c : total;
+  }
+  const uint64_t runlen = a.rank_list ? 1 : a.runlen;
   const uint64_t njobs = (total + runlen - 1) / runlen;
   const uint64_t G = (uint64_t)gridDim.x * BD;
   const uint64_t outer = (njobs + G - 1) / G;
@@ -497,29 +414,31 @@ __global__ void __launch_bounds__(256) eval_kernel(EvalArgs a) {
     uint32_t p[N];
 #pragma unroll
     for (int j = 0; j < N; ++j) p[j] = j;
+    uint64_t rend = a.re;
     if (jobok) {
       if (a.cfgs) {
 #pragma unroll
         for (int j = 0; j < N; ++j) p[j] = a.cfgs[rank * N + j];
       } else {
+        if (a.rank_list) {
+          rank = a.rank_list[job];
+          rend = rank + 1;
+        }
         colex_unrank<N>(s.binom, a.ns, rank, p);
       }
     }
     for (uint64_t t = 0; t < runlen; ++t) {
-      const bool have = jobok && rank < a.re;
+      const bool have = jobok && rank < rend;
       CfgOut r;
       if (have) {
         eval_config<N, FULL>(a, s, p, sorted_in, rank - a.rb, r);
         if (r.valid) ++valid_cnt;
         if (a.want_digest) {
-          uint64_t h = mix64(rank ^ ((uint64_t)r.lead_orig << 56));
+          uint32_t h = 0;
 #pragma unroll
-          for (int sl = 0; sl < NSLOT; ++sl) {
-            if (!slot_has<N>(sl)) continue;
-            h = mix64(h ^ (r.mom[sl].s1 + ((uint64_t)sl << 48)));
-            h = mix64(h ^ r.mom[sl].s2);
-          }
-          digest += h;
+          for (int sl = 0; sl < NSLOT; ++sl)
+            if (slot_has<N>(sl)) h = digest_fold(h, r.mom[sl].s1, r.mom[sl].s2);
+          digest += digest_final(rank, r.lead_orig, h);
         }
         if (FULL) {
           const uint64_t oi = rank - a.rb;
@@ -538,52 +457,27 @@ __global__ void __launch_bounds__(256) eval_kernel(EvalArgs a) {
       }
       if (topk) {
         uint64_t key[MAXOBJ];
-        bool pass[MAXOBJ];
-        bool any = false;
+        bool ok[MAXOBJ];
 #pragma unroll
         for (int o = 0; o < MAXOBJ; ++o) {
-          pass[o] = false;
+          ok[o] = false;
           key[o] = 0;
           if (o < a.n_obj && have) {
             const uint32_t kind = a.obj_kind[o], sl = a.obj_slot[o];
-            bool ok = true;
+            ok[o] = true;
             if (kind == OBJ_SCORE) {
-              ok = r.valid;
+              ok[o] = r.valid;
               key[o] = ~orderable_f64(r.score);
             } else {
               // `sl` is uniform: one scalar branch per slot keeps r.mom in
               // registers (a select chain here gets turned into scratch).
 #pragma unroll
-              for (int q = 0; q < NSLOT; ++q) {
-                if ((uint32_t)q == sl) {
-                  const Mom& m = r.mom[q];
-                  if (kind == OBJ_MEAN) {
-                    key[o] = m.s1;
-                  } else if (cov_nan(m)) {
-                    key[o] = ~0ull;
-                  } else {
-                    double rr = (double)mom_v(m) / ((double)m.s1 * (double)m.s1);
-                    key[o] = (uint64_t)__double_as_longlong(rr);
-                  }
-                }
-              }
+              for (int q = 0; q < NSLOT; ++q)
+                if ((uint32_t)q == sl) key[o] = kind == OBJ_MEAN ? r.mom[q].s1 : cov_key(r.mom[q]);
             }
-            pass[o] = ok && rec_lt(Rec{key[o], rank}, s.thr[o]);
-            any = any || pass[o];
           }
         }
-        if (__syncthreads_or(any)) {
-#pragma unroll
-          for (int o = 0; o < MAXOBJ; ++o) {
-            if (o >= a.n_obj) break;
-            if (pass[o] && rec_lt(Rec{key[o], rank}, s.thr[o])) {
-              int i = atomicAdd(s.cnt, 1);
-              s.cand[i] = Rec{key[o], rank};
-            }
-            __syncthreads();
-            if (*s.cnt > 0) topk_merge(s, o, a.K);
-          }
-        }
+        topk_step(s.tk, a.n_obj, a.K, key, ok, rank);
       }
       if (have && !a.cfgs) colex_next<N>(a.ns, p);
       ++rank;
@@ -597,7 +491,7 @@ __global__ void __launch_bounds__(256) eval_kernel(EvalArgs a) {
   if (topk) {
     __syncthreads();
     Rec* dst = a.out_top + (size_t)blockIdx.x * a.n_obj * KP;
-    for (uint32_t i = tid; i < (uint32_t)a.n_obj * KP; i += BD) dst[i] = s.top[i];
+    for (uint32_t i = tid; i < (uint32_t)a.n_obj * KP; i += BD) dst[i] = s.tk.top[i];
   }
 }
 

@@ -22,6 +22,10 @@ struct EvalArgs {
   int srv_sorted;  // srv ascending => colex positions are already in name order
   // work: explicit configs (positions, n per config) or colex ranks
   const uint32_t* cfgs;
+  // or an explicit device list of colex ranks whose length is read on the
+  // device (the fast sweep's deferred near-tie configs): [0, *rank_count)
+  const uint64_t* rank_list;
+  const unsigned long long* rank_count;
   uint64_t rb, re;  // [rb, re) ranks, or config indices when cfgs != null
   uint32_t runlen;  // consecutive ranks per lane job
   const uint64_t* binom;  // (ns+1) x (n+1)
@@ -64,6 +68,39 @@ struct SingleArgs {
   uint32_t* out_pos;
   int* err;
 };
+
+// ---- fast-path sweep (bote_sweep.hip)
+constexpr uint32_t FAST_BD = 256;
+struct FastArgs {
+  const uint2* cqt;  // client quads, column-major, column stride (cq_quads + 1) uint2
+  const uint2* rqt;  // region quads (rows = all regions), used when rq_separate
+  int rq_separate;
+  uint32_t R, cq_quads, rq_quads;
+  const uint32_t* srv;
+  uint32_t ns;
+  int srv_identity;  // srv[p] == p
+  uint32_t nc;
+  const uint64_t* binom;
+  uint64_t rb, re;
+  uint32_t runlen;
+  uint32_t s2_flush;  // quads per 32-bit sum-of-squares chunk
+  int want_score, p_int;
+  double p_fmean, p_emean;
+  int ft_metric;
+  int n_obj;
+  uint32_t obj_kind[MAXOBJ];
+  uint32_t obj_slot[MAXOBJ];
+  uint32_t K;
+  Rec* out_top;
+  unsigned long long* out_counters;
+  int want_digest;
+  uint64_t* queue;  // deferred near-tie configs (colex ranks)
+  unsigned long long* queue_count;
+  uint64_t queue_cap;
+};
+size_t fast_smem_bytes(const FastArgs& a, uint32_t n);
+int fast_occupancy(uint32_t n, size_t shm);
+hipError_t launch_fast(const FastArgs& a, uint32_t n, uint32_t grid, size_t shm, hipStream_t st);
 
 size_t eval_smem_bytes(const EvalArgs& a, uint32_t n, uint32_t bd, bool topk);
 int eval_occupancy(uint32_t n, bool full, uint32_t bd, size_t shm);

@@ -1,0 +1,541 @@
+// bote_sweep.hip — the fast-path sweep kernel (gfx950): exhaustive search over
+// colex ranks with a block top-K, for planets that meet the fast-path
+// preconditions checked on the host (bote_capi.hip, fast_eligible):
+//   * every latency <= 4095 (packed u16 keys: latency << 4 | member)
+//   * the server set is "simple": self latency 0, latency between two servers
+//     > 0 (a colocated client's nearest server is itself)
+//   * servers in name order, >= 2 clients, min_fairness_fpaxos_improv == 0
+// Anything else runs the generic kernel (bote_kernels.hip), which is also the
+// exact path for the rare configs this kernel defers (COV near-ties).
+//
+// Data layout in LDS (DESIGN.md "Data layout"):
+//   CQT[t][g]  uint2 = 4 x u16 (latency << 4) from clients 4g..4g+3 to region
+//              t; column stride (nq + 1) * 8 bytes, an odd number of 8-byte
+//              slots, so distinct columns spread over the ds_read_b64 banks.
+//   RQT        the same layout with ALL regions as the rows (== CQT when the
+//              client list is 0..R-1): L[a][b] = RQT[b][a >> 2].u16[a & 3].
+//   qtab       per lane and member: packed leaderless quorum latencies,
+//              plane-major [member][lane] (conflict-free).
+//
+// Per config (one lane; reference functions in bote_kernels.hip's header):
+// quorum latencies by sorting each member's off-diagonal distances; FPaxos
+// leader by exact-COV comparison (variance is shift invariant, so leader l's
+// V = nc*sum(L^2) - (sum L)^2 of its column, precomputed per position); the
+// Input leaderless keys by the packed client-quad loop; compute_score validity
+// by integer / f64-margin decisions; digest; block top-K.
+#include "bote_kernels.hpp"
+
+namespace bote {
+
+typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ us2 as_us2(uint32_t x) { return __builtin_bit_cast(us2, x); }
+__device__ __forceinline__ uint32_t as_u32(us2 x) { return __builtin_bit_cast(uint32_t, x); }
+
+constexpr uint32_t QSH = 10;  // log2(FAST_BD * 4): byte stride between qtab member planes
+static_assert((1u << QSH) == FAST_BD * 4, "qtab plane stride");
+
+struct FastSmem {
+  unsigned char* base;  // dynamic LDS base; byte offsets below are relative to it
+  uint32_t cqt, rqt, qtab;
+  uint32_t* srv;
+  uint32_t* cs1;
+  uint64_t* cs2;
+  double* vcol;
+  uint64_t* binom;
+  TopkLds tk;
+};
+
+__host__ __device__ inline size_t fast_layout(const FastArgs& a, int N, int NLW, size_t* off) {
+  size_t o = 0;
+  off[0] = o; o += (size_t)N * FAST_BD * NLW * 4;  // qtab first: offsets stay small
+  off[1] = o; o += (size_t)a.R * (a.cq_quads + 1) * 8;
+  off[2] = o; o += a.rq_separate ? (size_t)a.R * (a.rq_quads + 1) * 8 : 0;
+  off[3] = o; o += (size_t)a.ns * 4;  // srv
+  off[4] = o; o += (size_t)a.ns * 4;  // cs1
+  o = (o + 15) & ~(size_t)15;
+  off[5] = o; o += (size_t)a.ns * 8;                   // cs2
+  off[6] = o; o += (size_t)a.ns * 8;                   // vcol
+  off[7] = o; o += (size_t)(a.ns + 1) * (N + 1) * 8;  // binom
+  o = (o + 15) & ~(size_t)15;
+  off[8] = o; o += (size_t)a.n_obj * KP * 16;  // top
+  off[9] = o; o += (size_t)FAST_BD * 16;      // cand
+  off[10] = o; o += (size_t)KP * 16;          // tmp
+  off[11] = o; o += (size_t)MAXOBJ * 16;      // thr
+  off[12] = o; o += 16;                       // cnt
+  return o;
+}
+
+size_t fast_smem_bytes(const FastArgs& a, uint32_t n) {
+  size_t off[13];
+  int nl = 0;
+  switch (n) {
+#define NL_CASE(NN) case NN: nl = QCfg<NN>::NL; break;
+    NL_CASE(2) NL_CASE(3) NL_CASE(4) NL_CASE(5) NL_CASE(6) NL_CASE(7) NL_CASE(8) NL_CASE(9)
+    NL_CASE(10) NL_CASE(11) NL_CASE(12) NL_CASE(13) NL_CASE(14) NL_CASE(15) NL_CASE(16)
+#undef NL_CASE
+    default: return 0;
+  }
+  return fast_layout(a, (int)n, nl <= 2 ? 1 : 2, off);
+}
+
+template <int N>
+__device__ __forceinline__ uint32_t sel_u(const uint32_t (&arr)[N], uint32_t i) {
+  uint32_t r = 0;
+#pragma unroll
+  for (int j = 0; j < N; ++j) r |= arr[j] & (0u - (uint32_t)(i == (uint32_t)j));
+  return r;
+}
+
+__device__ __forceinline__ uint32_t ld16(const unsigned char* b, uint32_t off) { return *(const uint16_t*)(b + off); }
+__device__ __forceinline__ uint32_t ld32(const unsigned char* b, uint32_t off) { return *(const uint32_t*)(b + off); }
+__device__ __forceinline__ uint2 ld64(const unsigned char* b, uint32_t off) { return *(const uint2*)(b + off); }
+
+// ------------------------------------------------------------ hot loop ----
+// Input leaderless keys over client quads.  Per quad and member: one
+// ds_read_b64 (4 clients), a packed OR of the member index and a packed min
+// (v_pk_min_u16: ties go to the lower member = the lower name); per client:
+// one qtab read for the nearest member's quorum latencies; packed adds and
+// v_dot2_u32_u16 accumulate the sum and the sum of squares.  Squares are
+// accumulated in 32 bits and flushed to 64 bits every `flushQ` quads.
+template <int N, int NL>
+__device__ __forceinline__ void client_quads(const unsigned char* B, uint32_t cqt, uint32_t nq, uint32_t rem,
+                                             uint32_t flushQ, const uint32_t (&colT)[N], uint32_t qlane,
+                                             uint32_t (&S1)[NL], uint64_t (&S2)[NL]) {
+  const us2 ones = {1, 1};
+  uint32_t s2[NL];
+#pragma unroll
+  for (int t = 0; t < NL; ++t) {
+    S1[t] = 0;
+    S2[t] = 0;
+    s2[t] = 0;
+  }
+  uint32_t col[N];
+#pragma unroll
+  for (int j = 0; j < N; ++j) col[j] = cqt + colT[j];
+
+  auto quad = [&](uint32_t g8, uint32_t mlo, uint32_t mhi) {
+    uint2 w = ld64(B, col[0] + g8);
+    us2 lo = as_us2(w.x), hi = as_us2(w.y);
+#pragma unroll
+    for (int j = 1; j < N; ++j) {
+      w = ld64(B, col[j] + g8);
+      const us2 J = {(unsigned short)j, (unsigned short)j};
+      lo = __builtin_elementwise_min(lo, as_us2(w.x) | J);
+      hi = __builtin_elementwise_min(hi, as_us2(w.y) | J);
+    }
+    const uint32_t L = as_u32(lo), H = as_u32(hi);
+    // qtab sits at LDS offset 0, so qlane < 2^QSH and the member plane offset
+    // can be OR-ed in: (x << 10 & 0x3C00) | qlane -> v_lshlrev + v_and_or_b32
+    constexpr uint32_t QM = 15u << QSH;
+    const uint32_t q0 = ld32(B, ((L << QSH) & QM) | qlane);
+    const uint32_t q1 = ld32(B, ((L >> (16 - QSH)) & QM) | qlane);
+    const uint32_t q2 = ld32(B, ((H << QSH) & QM) | qlane);
+    const uint32_t q3 = ld32(B, ((H >> (16 - QSH)) & QM) | qlane);
+    const us2 dlo = lo >> (us2)4, dhi = hi >> (us2)4;
+    {
+      us2 a01 = dlo + as_us2(__builtin_amdgcn_perm(q1, q0, 0x05040100u));
+      us2 a23 = dhi + as_us2(__builtin_amdgcn_perm(q3, q2, 0x05040100u));
+      a01 = as_us2(as_u32(a01) & mlo);
+      a23 = as_us2(as_u32(a23) & mhi);
+      S1[0] = __builtin_amdgcn_udot2(a01, ones, S1[0], false);
+      S1[0] = __builtin_amdgcn_udot2(a23, ones, S1[0], false);
+      s2[0] = __builtin_amdgcn_udot2(a01, a01, s2[0], false);
+      s2[0] = __builtin_amdgcn_udot2(a23, a23, s2[0], false);
+    }
+    if (NL >= 2) {
+      us2 a01 = dlo + as_us2(__builtin_amdgcn_perm(q1, q0, 0x07060302u));
+      us2 a23 = dhi + as_us2(__builtin_amdgcn_perm(q3, q2, 0x07060302u));
+      a01 = as_us2(as_u32(a01) & mlo);
+      a23 = as_us2(as_u32(a23) & mhi);
+      S1[NL >= 2 ? 1 : 0] = __builtin_amdgcn_udot2(a01, ones, S1[NL >= 2 ? 1 : 0], false);
+      S1[NL >= 2 ? 1 : 0] = __builtin_amdgcn_udot2(a23, ones, S1[NL >= 2 ? 1 : 0], false);
+      s2[NL >= 2 ? 1 : 0] = __builtin_amdgcn_udot2(a01, a01, s2[NL >= 2 ? 1 : 0], false);
+      s2[NL >= 2 ? 1 : 0] = __builtin_amdgcn_udot2(a23, a23, s2[NL >= 2 ? 1 : 0], false);
+    }
+    if (NL == 3) {
+      const uint32_t P2 = (uint32_t)N << QSH;  // second plane follows the first
+      const uint32_t r0 = ld32(B, qlane + P2 + ((L & 15u) << QSH));
+      const uint32_t r1 = ld32(B, qlane + P2 + (((L >> 16) & 15u) << QSH));
+      const uint32_t r2 = ld32(B, qlane + P2 + ((H & 15u) << QSH));
+      const uint32_t r3 = ld32(B, qlane + P2 + (((H >> 16) & 15u) << QSH));
+      us2 a01 = dlo + as_us2(__builtin_amdgcn_perm(r1, r0, 0x05040100u));
+      us2 a23 = dhi + as_us2(__builtin_amdgcn_perm(r3, r2, 0x05040100u));
+      a01 = as_us2(as_u32(a01) & mlo);
+      a23 = as_us2(as_u32(a23) & mhi);
+      S1[NL - 1] = __builtin_amdgcn_udot2(a01, ones, S1[NL - 1], false);
+      S1[NL - 1] = __builtin_amdgcn_udot2(a23, ones, S1[NL - 1], false);
+      s2[NL - 1] = __builtin_amdgcn_udot2(a01, a01, s2[NL - 1], false);
+      s2[NL - 1] = __builtin_amdgcn_udot2(a23, a23, s2[NL - 1], false);
+    }
+  };
+  auto flush = [&]() {
+#pragma unroll
+    for (int t = 0; t < NL; ++t) {
+      S2[t] += s2[t];
+      s2[t] = 0;
+    }
+  };
+
+  for (uint32_t g0 = 0; g0 < nq; g0 += flushQ) {
+    const uint32_t ge = min(nq, g0 + flushQ);
+    uint32_t g = g0;
+    for (; g + 4 <= ge; g += 4) {
+      quad(g * 8 + 0, ~0u, ~0u);
+      quad(g * 8 + 8, ~0u, ~0u);
+      quad(g * 8 + 16, ~0u, ~0u);
+      quad(g * 8 + 24, ~0u, ~0u);
+    }
+    for (; g < ge; ++g) quad(g * 8, ~0u, ~0u);
+    flush();
+  }
+  if (rem) {
+    const uint32_t mlo = rem >= 2 ? ~0u : 0x0000FFFFu, mhi = rem == 3 ? 0x0000FFFFu : 0u;
+    quad(nq * 8, mlo, mhi);
+    flush();
+  }
+}
+
+// ---------------------------------------------------------- the kernel ----
+template <int N>
+__global__ void __launch_bounds__(FAST_BD, 4) sweep_fast_kernel(FastArgs a) {
+  using QC = QCfg<N>;
+  constexpr int NL = QC::NL;
+  constexpr int NLW = NL <= 2 ? 1 : 2;
+  constexpr int P = Pow2<N - 1>::v;  // off-diagonal row values, padded
+  extern __shared__ __align__(16) unsigned char smem[];
+  size_t off[13];
+  fast_layout(a, N, NLW, off);
+  FastSmem s;
+  s.base = smem;
+  s.qtab = (uint32_t)off[0];
+  s.cqt = (uint32_t)off[1];
+  s.rqt = a.rq_separate ? (uint32_t)off[2] : (uint32_t)off[1];
+  s.srv = (uint32_t*)(smem + off[3]);
+  s.cs1 = (uint32_t*)(smem + off[4]);
+  s.cs2 = (uint64_t*)(smem + off[5]);
+  s.vcol = (double*)(smem + off[6]);
+  s.binom = (uint64_t*)(smem + off[7]);
+  s.tk.top = (Rec*)(smem + off[8]);
+  s.tk.cand = (Rec*)(smem + off[9]);
+  s.tk.tmp = (Rec*)(smem + off[10]);
+  s.tk.thr = (Rec*)(smem + off[11]);
+  s.tk.cnt = (int*)(smem + off[12]);
+  const uint32_t tid = threadIdx.x;
+  const unsigned char* B = smem;
+
+  // ---- stage: quad matrices, server list, binomials; then per-position sums
+  {
+    const uint32_t cw = a.R * (a.cq_quads + 1) * 2;  // 32-bit words
+    const uint32_t* src = (const uint32_t*)a.cqt;
+    uint32_t* dst = (uint32_t*)(smem + s.cqt);
+    for (uint32_t i = tid; i < cw; i += FAST_BD) dst[i] = src[i];
+    if (a.rq_separate) {
+      const uint32_t rw = a.R * (a.rq_quads + 1) * 2;
+      const uint32_t* rs = (const uint32_t*)a.rqt;
+      uint32_t* rd = (uint32_t*)(smem + s.rqt);
+      for (uint32_t i = tid; i < rw; i += FAST_BD) rd[i] = rs[i];
+    }
+  }
+  for (uint32_t i = tid; i < a.ns; i += FAST_BD) s.srv[i] = a.srv[i];
+  for (uint32_t i = tid; i < (a.ns + 1) * (N + 1); i += FAST_BD) s.binom[i] = a.binom[i];
+  topk_init(s.tk, a.n_obj);
+  __syncthreads();
+  const uint32_t cstride = (a.cq_quads + 1) * 8;  // bytes per CQT column
+  const uint32_t rstride = (a.rq_quads + 1) * 8;
+  for (uint32_t i = tid; i < a.ns; i += FAST_BD) {
+    const uint32_t col = s.cqt + s.srv[i] * cstride;
+    uint64_t c1 = 0, c2 = 0;
+    for (uint32_t c = 0; c < a.nc; ++c) {
+      uint64_t v = ld16(B, col + (c >> 2) * 8 + (c & 3) * 2) >> LAT_SHIFT;
+      c1 += v;
+      c2 += v * v;
+    }
+    s.cs1[i] = (uint32_t)c1;
+    s.cs2[i] = c2;
+    s.vcol[i] = (double)((uint64_t)a.nc * c2 - c1 * c1);  // exact: < 2^53
+  }
+  __syncthreads();
+
+  const uint32_t nc = a.nc, nq = nc >> 2, rem = nc & 3;
+  const uint32_t qlane = s.qtab + tid * 4;
+  const uint64_t total = a.re - a.rb;
+  const uint64_t runlen = a.runlen;
+  const uint64_t njobs = (total + runlen - 1) / runlen;
+  const uint64_t G = (uint64_t)gridDim.x * FAST_BD;
+  const uint64_t outer = (njobs + G - 1) / G;
+  const double pnc1 = a.p_fmean * (double)nc, pnc2 = a.p_emean * (double)nc;
+  uint64_t valid_cnt = 0, digest = 0;
+
+  for (uint64_t it = 0; it < outer; ++it) {
+    const uint64_t job = it * G + (uint64_t)blockIdx.x * FAST_BD + tid;
+    const bool jobok = job < njobs;
+    uint64_t rank = a.rb + job * runlen;
+    uint32_t p[N];
+#pragma unroll
+    for (int j = 0; j < N; ++j) p[j] = j;
+    if (jobok) colex_unrank<N>(s.binom, a.ns, rank, p);
+    for (uint64_t tt = 0; tt < runlen; ++tt) {
+      bool have = jobok && rank < a.re;
+      uint64_t key[MAXOBJ];
+      bool ok[MAXOBJ];
+#pragma unroll
+      for (int o = 0; o < MAXOBJ; ++o) {
+        key[o] = 0;
+        ok[o] = false;
+      }
+      if (have) {
+        // ---- members (positions ascending == names ascending)
+        uint32_t colT[N], colR[N], rowq[N];
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+          const uint32_t r = a.srv_identity ? p[j] : s.srv[p[j]];
+          colT[j] = r * cstride;
+          colR[j] = s.rqt + r * rstride;
+          rowq[j] = (r >> 2) * 8 + (r & 3) * 2;
+        }
+        // ---- Q phase: sorted off-diagonal distances of each member's row
+        uint32_t Q2[N], Q3[N];
+        uint32_t cS1[NL], cS2[NL];
+#pragma unroll
+        for (int t = 0; t < NL; ++t) cS1[t] = cS2[t] = 0;
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+          uint32_t v[P];
+          int t = 0;
+#pragma unroll
+          for (int k = 0; k < N; ++k)
+            if (k != j) v[t++] = ld16(B, colR[k] + rowq[j]) >> LAT_SHIFT;
+#pragma unroll
+          for (int k = N - 1; k < P; ++k) v[k] = 0xFFFFFFFFu;
+          sort_network<P>(v);
+          // the row's q-th smallest (self = 0 first) is the (q-1)-th off-diagonal
+          Q2[j] = v[0];
+          Q3[j] = QC::maxf >= 2 ? v[QC::maxf >= 2 ? 1 : 0] : 0u;
+          uint32_t ql[NL];
+#pragma unroll
+          for (int t2 = 0; t2 < NL; ++t2) {
+            ql[t2] = v[QC::lq(t2) - 2];
+            cS1[t2] += ql[t2];
+            cS2[t2] += ql[t2] * ql[t2];
+          }
+          *(uint32_t*)(smem + qlane + ((uint32_t)j << QSH)) = ql[0] | (NL >= 2 ? ql[NL >= 2 ? 1 : 0] << 16 : 0u);
+          if (NL == 3) *(uint32_t*)(smem + qlane + ((uint32_t)(N + j) << QSH)) = ql[NL - 1];
+          // one member row at a time: keeps the row's reads and sort network
+          // from being interleaved with the next rows (register pressure)
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        // ---- FPaxos leader (f = 1, q = 2, min COV, first in config order)
+        uint32_t bi = 0;
+        bool amb = false;
+        {
+          uint32_t c1 = s.cs1[p[0]];
+          double bS = (double)(c1 + nc * Q2[0]);
+          bS = bS * bS;
+          double bV = s.vcol[p[0]];
+#pragma unroll
+          for (int l = 1; l < N; ++l) {
+            const double V = s.vcol[p[l]];
+            double S = (double)(s.cs1[p[l]] + nc * Q2[l]);
+            S = S * S;
+            const double x = V * bS, y = bV * S;  // cov_l^2 < cov_best^2  <=>  x < y
+            const bool zero = (V == 0.0) && (bV == 0.0);
+            const double d = x - y, tol = 0x1p-32 * fmax(x, y);
+            if (!zero && fabs(d) <= tol) amb = true;
+            if (!zero && d < -tol) {
+              bi = l;
+              bS = S;
+              bV = V;
+            }
+          }
+        }
+        if (amb) {
+          // defer to the exact generic kernel (see bote_sweep_launch)
+          unsigned long long q = atomicAdd(a.queue_count, 1ull);
+          if (q < a.queue_cap) a.queue[q] = rank;
+          have = false;
+        }
+        if (have) {
+          const uint32_t lp = sel_u(p, bi), lq2 = sel_u(Q2, bi), lq3 = sel_u(Q3, bi);
+          const uint32_t lcol = sel_u(colR, bi);
+          Mom mom[NSLOT];
+          // Input leaderless: the hot loop (first, so little is live across it)
+          {
+            uint32_t S1[NL];
+            uint64_t S2[NL];
+            client_quads<N, NL>(B, s.cqt, nq, rem, a.s2_flush, colT, qlane, S1, S2);
+            mom[SLOT_AF1] = Mom{S1[QC::idx_a1], S2[QC::idx_a1], nc};
+            mom[SLOT_AF2] = Mom{S1[QC::idx_a2], S2[QC::idx_a2], nc};
+            mom[SLOT_E] = Mom{S1[QC::idx_e], S2[QC::idx_e], nc};
+          }
+          // Input FPaxos: moments from the leader column's sums
+          {
+            const uint64_t c1 = s.cs1[lp], c2 = s.cs2[lp];
+            uint64_t q = lq2;
+            mom[SLOT_FF1] = Mom{c1 + (uint64_t)nc * q, c2 + 2ull * q * c1 + (uint64_t)nc * q * q, nc};
+            q = lq3;
+            mom[SLOT_FF2] = Mom{c1 + (uint64_t)nc * q, c2 + 2ull * q * c1 + (uint64_t)nc * q * q, nc};
+          }
+          // Colocated: leaderless values are the members' own quorum latencies;
+          // FPaxos reads the leader's column of the config submatrix.
+          {
+            uint32_t f1 = 0, f1s = 0, f2 = 0, f2s = 0;
+#pragma unroll
+            for (int k = 0; k < N; ++k) {
+              const uint32_t v = ld16(B, lcol + rowq[k]) >> LAT_SHIFT;
+              const uint32_t x1 = v + lq2, x2 = v + lq3;
+              f1 += x1;
+              f1s += x1 * x1;
+              f2 += x2;
+              f2s += x2 * x2;
+            }
+            mom[5 + SLOT_FF1] = Mom{f1, f1s, (uint32_t)N};
+            mom[5 + SLOT_FF2] = Mom{f2, f2s, (uint32_t)N};
+            mom[5 + SLOT_AF1] = Mom{cS1[QC::idx_a1], cS2[QC::idx_a1], (uint32_t)N};
+            mom[5 + SLOT_AF2] = Mom{cS1[QC::idx_a2], cS2[QC::idx_a2], (uint32_t)N};
+            mom[5 + SLOT_E] = Mom{cS1[QC::idx_e], cS2[QC::idx_e], (uint32_t)N};
+          }
+          // ---- compute_score validity and score (search.rs:421-472)
+          bool valid = false;
+          double score = 0.0;
+          if (a.want_score) {
+            valid = true;
+            const int fcap = min(N / 2, a.ft_metric);
+#pragma unroll
+            for (int f = 1; f <= 2; ++f) {
+              if (f > fcap) break;
+              const Mom& ma = mom[f == 1 ? SLOT_AF1 : SLOT_AF2];
+              const Mom& mf = mom[f == 1 ? SLOT_FF1 : SLOT_FF2];
+              // fmi >= p1: exact in integers unless the sums meet exactly
+              const double D = (double)(int64_t)(mf.s1 - ma.s1);
+              bool mok;
+              if (a.p_int && D != pnc1) mok = D > pnc1;
+              else mok = (mom_mean(mf) - mom_mean(ma)) >= a.p_fmean;
+              valid = valid && mok;
+              if (valid) {
+                // cov_f >= cov_a  <=>  V_f * S1_a^2 >= V_a * S1_f^2
+                const double Vf = s.vcol[lp];
+                const double Va = (double)mom_v(ma);
+                const double sa = (double)ma.s1 * (double)ma.s1, sf = (double)mf.s1 * (double)mf.s1;
+                const double x = Vf * sa, y = Va * sf;
+                if (!(Vf == 0.0 && Va == 0.0)) {
+                  const double d = x - y, tol = 0x1p-32 * fmax(x, y);
+                  if (fabs(d) <= tol) amb = true;
+                  valid = valid && d > 0.0;
+                }
+              }
+              if (N == 11 || N == 13) {
+                const double De = (double)(int64_t)(mom[SLOT_E].s1 - ma.s1);
+                bool eok;
+                if (a.p_int && De != pnc2) eok = De > pnc2;
+                else eok = (mom_mean(mom[SLOT_E]) - mom_mean(ma)) >= a.p_emean;
+                valid = valid && eok;
+              }
+            }
+            if (valid && !amb) {
+              const double me = mom_mean(mom[SLOT_E]);
+#pragma unroll
+              for (int f = 1; f <= 2; ++f) {
+                if (f > fcap) break;
+                const double mA = mom_mean(mom[f == 1 ? SLOT_AF1 : SLOT_AF2]);
+                const double fmi = mom_mean(mom[f == 1 ? SLOT_FF1 : SLOT_FF2]) - mA;
+                const double emi = me - mA;
+                double t = 30.0 * emi;
+                t = fmi + t;
+                score = score + t;
+              }
+            }
+          }
+          if (amb) {
+            unsigned long long q = atomicAdd(a.queue_count, 1ull);
+            if (q < a.queue_cap) a.queue[q] = rank;
+            have = false;
+          } else {
+            if (valid) ++valid_cnt;
+            if (a.want_digest) {
+              uint32_t h = 0;
+#pragma unroll
+              for (int sl = 0; sl < NSLOT; ++sl)
+                if (QC::maxf >= 2 || (sl % 5 != SLOT_AF2 && sl % 5 != SLOT_FF2))
+                  h = digest_fold(h, mom[sl].s1, mom[sl].s2);
+              digest += digest_final(rank, bi, h);
+            }
+            // ---- objective keys
+#pragma unroll
+            for (int o = 0; o < MAXOBJ; ++o) {
+              if (o >= a.n_obj) break;
+              const uint32_t kind = a.obj_kind[o], sl = a.obj_slot[o];
+              if (kind == OBJ_SCORE) {
+                ok[o] = valid;
+                key[o] = ~orderable_f64(score);
+                continue;
+              }
+#pragma unroll
+              for (int q = 0; q < NSLOT; ++q) {
+                if ((uint32_t)q != sl) continue;
+                const Mom& m = mom[q];
+                if (kind == OBJ_MEAN) {
+                  ok[o] = true;
+                  key[o] = m.s1;
+                } else {
+                  // COV key fl(V / S1^2): divide only when it may beat the threshold
+                  const uint64_t tk = s.tk.thr[o].key;
+                  const double V = (double)mom_v(m), S = (double)m.s1 * (double)m.s1;
+                  const bool maybe = tk == ~0ull || V <= __longlong_as_double((long long)tk) * S * (1.0 + 0x1p-40);
+                  if (maybe) {
+                    ok[o] = true;
+                    key[o] = cov_key(m);
+                  }
+                }
+              }
+            }
+          }
+        }
+      }
+      topk_step(s.tk, a.n_obj, a.K, key, ok, rank);
+      if (jobok && rank < a.re) colex_next<N>(a.ns, p);
+      ++rank;
+    }
+  }
+  if (valid_cnt) atomicAdd(&a.out_counters[0], (unsigned long long)valid_cnt);
+  if (digest) atomicAdd(&a.out_counters[1], (unsigned long long)digest);
+  __syncthreads();
+  Rec* dst = a.out_top + (size_t)blockIdx.x * a.n_obj * KP;
+  for (uint32_t i = tid; i < (uint32_t)a.n_obj * KP; i += FAST_BD) dst[i] = s.tk.top[i];
+}
+
+// ------------------------------------------------------------- launcher ---
+template <int N>
+static hipError_t launch_fast_n(const FastArgs& a, uint32_t grid, size_t shm, hipStream_t st) {
+  auto k = sweep_fast_kernel<N>;
+  hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k, dim3(grid), dim3(FAST_BD), shm, st, a);
+  return hipGetLastError();
+}
+
+int fast_occupancy(uint32_t n, size_t shm) {
+  int nb = 0;
+  const void* k = nullptr;
+  switch (n) {
+#define OCC_CASE(NN) case NN: k = (const void*)sweep_fast_kernel<NN>; break;
+    OCC_CASE(2) OCC_CASE(3) OCC_CASE(4) OCC_CASE(5) OCC_CASE(6) OCC_CASE(7) OCC_CASE(8) OCC_CASE(9)
+    OCC_CASE(10) OCC_CASE(11) OCC_CASE(12) OCC_CASE(13) OCC_CASE(14) OCC_CASE(15) OCC_CASE(16)
+#undef OCC_CASE
+    default: return 0;
+  }
+  if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm) != hipSuccess) return 1;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, (int)FAST_BD, shm) != hipSuccess) return 1;
+  return nb > 0 ? nb : 1;
+}
+
+hipError_t launch_fast(const FastArgs& a, uint32_t n, uint32_t grid, size_t shm, hipStream_t st) {
+  switch (n) {
+#define FS_CASE(NN) case NN: return launch_fast_n<NN>(a, grid, shm, st);
+    FS_CASE(2) FS_CASE(3) FS_CASE(4) FS_CASE(5) FS_CASE(6) FS_CASE(7) FS_CASE(8) FS_CASE(9)
+    FS_CASE(10) FS_CASE(11) FS_CASE(12) FS_CASE(13) FS_CASE(14) FS_CASE(15) FS_CASE(16)
+#undef FS_CASE
+    default: return hipErrorInvalidValue;
+  }
+}
+
+}  // namespace bote

@@ -502,18 +502,20 @@ uint64_t mix64(uint64_t z) {
   z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
   return z ^ (z >> 31);
 }
-// Order-independent per-config digest shared with the GPU path:
-// mix64 over (rank, leader position, per-slot sum and sum of squares).
+// Order-independent per-config digest shared with the GPU path (DESIGN.md
+// "Digest"): a 32-bit fold of every present slot's exact sum and sum of
+// squares, then one mix64 with the rank and the leader position.
 uint64_t config_digest(uint64_t rank, const ProtocolStats& st) {
-  uint64_t h = mix64(rank ^ ((uint64_t)st.leader_pos << 56));
+  uint32_t h = 0;
   for (int s = 0; s < NKEYS; ++s) {
     if (!st.has[s]) continue;
     uint64_t s1, c;
     st.h[s].sum_and_count(s1, c);
-    h = mix64(h ^ (s1 + ((uint64_t)s << 48)));
-    h = mix64(h ^ st.h[s].sumsq());
+    uint64_t s2 = st.h[s].sumsq();
+    h = (h ^ (uint32_t)s1) * 0x9E3779B1u;
+    h = (h ^ (uint32_t)(s2 ^ (s2 >> 32))) * 0x85EBCA77u;
   }
-  return h;
+  return mix64(rank ^ ((uint64_t)st.leader_pos << 56) ^ ((uint64_t)h << 24));
 }
 
 thread_local std::string g_err;

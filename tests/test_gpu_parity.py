@@ -336,3 +336,66 @@ def test_r128_n6_subrange_and_max_latency():
     s16 = np.arange(16, dtype=np.uint32)
     cfg = np.array([_lib.colex_unrank(r, 9, 16) for r in range(0, _lib.binomial(16, 9), 7)], dtype=np.uint32)
     _check_eval(qo, DevicePlanet(q), s16, s16, 9, cfg)
+
+
+# ------------------------------------------------ fast path vs generic ----
+def _sweep(dp, srv, cli, n, rb, re, K=100, ranking=DEFAULT_RANKING, generic=False):
+    if generic:
+        os.environ["BOTE_FORCE_GENERIC"] = "1"
+    try:
+        sw = Sweep(dp, srv, cli, n, DEFAULT_OBJECTIVES, K=K, ranking=ranking, digest=True)
+    finally:
+        os.environ.pop("BOTE_FORCE_GENERIC", None)
+    assert sw.is_fast() == (not generic)
+    sw.launch(rb, re)
+    return sw.result()
+
+
+def test_fast_path_equals_generic_path():
+    p = Planet.synthetic(64)
+    dp = DevicePlanet(p)
+    srv = np.arange(64, dtype=np.uint32)
+    for n, rb, re in ((7, 10_000_000, 12_000_000), (6, 0, 3_000_000), (4, 0, _lib.binomial(64, 4))):
+        a = _sweep(dp, srv, srv, n, rb, re)
+        b = _sweep(dp, srv, srv, n, rb, re, generic=True)
+        assert (a.valid, a.digest, a.tops) == (b.valid, b.digest, b.tops)
+    # a client subset (separate region-quad matrix) and a ragged client count
+    g = Planet.new()
+    gdp = DevicePlanet(g)
+    gs = np.arange(g.R, dtype=np.uint32)
+    for cli in (np.array([3, 1, 4, 15, 9, 2, 6], np.uint32), np.arange(0, 20, 2, dtype=np.uint32)):
+        for n in (3, 5, 8):
+            a = _sweep(gdp, gs, cli, n, 0, _lib.binomial(g.R, n))
+            b = _sweep(gdp, gs, cli, n, 0, _lib.binomial(g.R, n), generic=True)
+            assert (a.valid, a.digest, a.tops) == (b.valid, b.digest, b.tops)
+
+
+def test_fast_path_deferral_equidistant():
+    """Every FPaxos leader ties exactly: the fast kernel defers every config
+    to the exact generic kernel; results still match the oracle."""
+    regions, p = Planet.equidistant(10, 12)
+    dp = DevicePlanet(p)
+    o = O.OraclePlanet.of(p)
+    srv = np.arange(p.R, dtype=np.uint32)
+    rp = RankingParams.new(0, 0, 0, 0, 3, 13, FTMetric.F1F2)
+    for n in (3, 5):
+        total = _lib.binomial(p.R, n)
+        got = _sweep(dp, srv, srv, n, 0, total, ranking=rp)
+        tops, valid, digest = _oracle_sweep(o, srv, srv, n, 0, total, DEFAULT_OBJECTIVES, 100, rp)
+        assert (got.valid, got.digest) == (valid, digest)
+        assert got.tops == [list(t) for t in tops]
+
+
+def test_fast_path_deferral_overflow():
+    """More deferred configs than the queue holds: the range is recomputed on
+    the generic path before results are returned."""
+    regions, p = Planet.equidistant(7, 48)
+    dp = DevicePlanet(p)
+    o = O.OraclePlanet.of(p)
+    srv = np.arange(p.R, dtype=np.uint32)
+    total = _lib.binomial(p.R, 5)
+    assert total > (1 << 20)
+    got = _sweep(dp, srv, srv, 5, 0, total)
+    tops, valid, digest = _oracle_sweep(o, srv, srv, 5, 0, total, DEFAULT_OBJECTIVES, 100, DEFAULT_RANKING)
+    assert (got.valid, got.digest) == (valid, digest)
+    assert got.tops == [list(t) for t in tops]
