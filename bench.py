@@ -165,7 +165,8 @@ def main():
             "roofline": {"bound": "valu", "achieved": achieved, "peak": VALU_PEAK_TOPS, "unit": "Tops/s",
                          "frac": achieved / VALU_PEAK_TOPS, "traffic": traffic,
                          "work_per_config": W, "kernel_ms_avg": kavg_ms,
-                         "kernel": "eval_kernel<N,false> (bote_kernels.hip)"},
+                         "kernel": ("sweep_fast_kernel<N> (bote_sweep.hip)" if sweep.is_fast()
+                                    else "eval_kernel<N,false> (bote_kernels.hip)")},
             "result_check": {"valid": res.valid, "digest": res.digest,
                              "top_score_rank": res.tops[0][0][1] if res.tops[0] else None},
         }

@@ -13,7 +13,8 @@ import subprocess
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libbote_hip.so")
+# BOTE_LIB_PATH: an alternative in-tree build for A/B timing experiments
+LIB_PATH = os.environ.get("BOTE_LIB_PATH") or os.path.join(HERE, "lib", "libbote_hip.so")
 CSRC = os.path.join(HERE, "csrc")
 INCLUDE_H = os.path.join(os.path.dirname(HERE), "include", "bote_hip.h")
 

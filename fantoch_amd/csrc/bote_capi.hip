@@ -573,6 +573,8 @@ int bote_sweep_create(const bote_planet* p, const uint32_t* servers, uint32_t ns
     f.queue = s->queue.as<uint64_t>();
     f.queue_count = s->qcount.as<unsigned long long>();
     f.queue_cap = QUEUE_CAP;
+    const char* abl = getenv("BOTE_ABLATE");  // timing diagnostics only
+    f.ablate = abl ? (uint32_t)strtoul(abl, nullptr, 0) : 0u;
     s->fshm = bote::fast_smem_bytes(f, n);
     if (s->fshm > device_max_lds(p->device)) {
       s->fast = false;
@@ -580,7 +582,8 @@ int bote_sweep_create(const bote_planet* p, const uint32_t* servers, uint32_t ns
       s->fgrid = (uint32_t)(device_cus(p->device) * bote::fast_occupancy(n, s->fshm));
     }
   }
-  const uint32_t lists = s->fast ? s->fgrid + s->xgrid : s->grid;
+  // the generic path may also run on a fast sweep (overflow recompute)
+  const uint32_t lists = s->fast ? std::max(s->grid, s->fgrid + s->xgrid) : s->grid;
   size_t top_bytes = (size_t)lists * std::max<uint32_t>(n_obj, 1) * bote::KP * 16;
   size_t tmp_bytes = (size_t)((lists + 7) / 8) * std::max<uint32_t>(n_obj, 1) * bote::KP * 16;
   if (s->top.alloc(top_bytes) != hipSuccess || s->tmp0.alloc(tmp_bytes) != hipSuccess ||

@@ -275,11 +275,11 @@ namespace bote {
 // record.  A config enters the candidate buffer only if it beats thr[o]; the
 // block merges candidates one objective at a time (bitonic sort + merge path).
 struct TopkLds {
-  Rec* top;   // MAXOBJ * KP
-  Rec* cand;  // blockDim.x
+  Rec* top;   // n_obj * KP
+  Rec* cand;  // blockDim.x (warm-up buffer, or MAXOBJ segments of SEG in batched mode)
   Rec* tmp;   // KP
   Rec* thr;   // MAXOBJ
-  int* cnt;
+  int* cnt;   // 1 + MAXOBJ counters (48 bytes reserved)
 };
 
 __device__ inline int lower_bound_rec(const Rec* a, int n, const Rec& x) {
@@ -302,25 +302,28 @@ __device__ inline int upper_bound_rec(const Rec* a, int n, const Rec& x) {
 __device__ inline void topk_init(const TopkLds& t, int n_obj) {
   for (uint32_t i = threadIdx.x; i < (uint32_t)n_obj * KP; i += blockDim.x) t.top[i] = rec_max();
   if (threadIdx.x < MAXOBJ) t.thr[threadIdx.x] = rec_max();
-  if (threadIdx.x == 0) *t.cnt = 0;
+  if (threadIdx.x <= MAXOBJ) t.cnt[threadIdx.x] = 0;  // [0] warm-up buffer, [1+o] segments
 }
 
-// Merge the candidate buffer (*t.cnt entries) into objective o's list.
+// Merge the candidate buffer (*t.cnt unsorted entries) into objective o's
+// list by ranks: every record's output slot is the number of records of the
+// other sequence below it plus its rank in its own.  Records are unique (one
+// per config and objective), padding records only fill the tail.  O(n) per
+// thread; after warm-up n is a handful, so this beats sorting the buffer.
 __device__ inline void topk_merge(const TopkLds& t, int o, uint32_t K) {
-  const int BD = blockDim.x, tid = threadIdx.x;
-  const int n = *t.cnt;
-  if (tid >= n) t.cand[tid] = rec_max();
-  __syncthreads();
-  block_bitonic(t.cand, BD);
+  const int tid = threadIdx.x;
+  const int n = *t.cnt;  // read after the caller's barrier: uniform
   Rec* top = t.top + o * KP;
   if (tid < KP) {
-    Rec x = top[tid];
-    int r = tid + lower_bound_rec(t.cand, BD, x);
+    const Rec x = top[tid];
+    int r = tid;
+    for (int j = 0; j < n; ++j) r += rec_lt(t.cand[j], x);
     if (r < KP) t.tmp[r] = x;
   }
-  {
-    Rec y = t.cand[tid];
-    int r = tid + upper_bound_rec(top, KP, y);
+  if (tid < n) {
+    const Rec y = t.cand[tid];
+    int r = lower_bound_rec(top, KP, y);
+    for (int j = 0; j < n; ++j) r += rec_lt(t.cand[j], y);
     if (r < KP) t.tmp[r] = y;
   }
   __syncthreads();

@@ -51,7 +51,7 @@ __host__ __device__ inline size_t smem_layout(const EvalArgs& a, int N, int NLW,
   off[7] = o; o += topk ? (size_t)BD * 16 : 0;
   off[8] = o; o += topk ? (size_t)KP * 16 : 0;
   off[9] = o; o += topk ? (size_t)MAXOBJ * 16 : 0;
-  off[10] = o; o += 16;
+  off[10] = o; o += 48;
   return o;
 }
 

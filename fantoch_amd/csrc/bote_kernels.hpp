@@ -97,6 +97,9 @@ struct FastArgs {
   uint64_t* queue;  // deferred near-tie configs (colex ranks)
   unsigned long long* queue_count;
   uint64_t queue_cap;
+  // timing diagnostics only (env BOTE_ABLATE; results are wrong when set):
+  // 1 skip client loop, 2 skip Q phase, 4 skip top-K step, 8 skip score, 16 skip digest
+  uint32_t ablate;
 };
 size_t fast_smem_bytes(const FastArgs& a, uint32_t n);
 int fast_occupancy(uint32_t n, size_t shm);

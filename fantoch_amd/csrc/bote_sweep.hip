@@ -25,6 +25,10 @@
 // by integer / f64-margin decisions; digest; block top-K.
 #include "bote_kernels.hpp"
 
+#ifndef BOTE_QROW_BARRIER
+#define BOTE_QROW_BARRIER 1
+#endif
+
 namespace bote {
 
 typedef unsigned short us2 __attribute__((ext_vector_type(2)));
@@ -61,7 +65,7 @@ __host__ __device__ inline size_t fast_layout(const FastArgs& a, int N, int NLW,
   off[9] = o; o += (size_t)FAST_BD * 16;      // cand
   off[10] = o; o += (size_t)KP * 16;          // tmp
   off[11] = o; o += (size_t)MAXOBJ * 16;      // thr
-  off[12] = o; o += 16;                       // cnt
+  off[12] = o; o += 48;                       // cnt[1 + MAXOBJ]
   return o;
 }
 
@@ -102,6 +106,7 @@ __device__ __forceinline__ void client_quads(const unsigned char* B, uint32_t cq
                                              uint32_t flushQ, const uint32_t (&colT)[N], uint32_t qlane,
                                              uint32_t (&S1)[NL], uint64_t (&S2)[NL]) {
   const us2 ones = {1, 1};
+  constexpr int NQ = NL == 3 ? 8 : 4;  // qtab words per quad
   uint32_t s2[NL];
 #pragma unroll
   for (int t = 0; t < NL; ++t) {
@@ -113,60 +118,68 @@ __device__ __forceinline__ void client_quads(const unsigned char* B, uint32_t cq
 #pragma unroll
   for (int j = 0; j < N; ++j) col[j] = cqt + colT[j];
 
-  auto quad = [&](uint32_t g8, uint32_t mlo, uint32_t mhi) {
-    uint2 w = ld64(B, col[0] + g8);
-    us2 lo = as_us2(w.x), hi = as_us2(w.y);
+  // stage 1: the quad's N member columns
+  auto load = [&](uint32_t g8, uint2 (&w)[N]) {
+#pragma unroll
+    for (int j = 0; j < N; ++j) w[j] = ld64(B, col[j] + g8);
+  };
+  // stage 2: nearest member per client (packed min of latency<<4 | member)
+  auto nearest = [&](const uint2 (&w)[N], us2& lo, us2& hi) {
+    lo = as_us2(w[0].x);
+    hi = as_us2(w[0].y);
 #pragma unroll
     for (int j = 1; j < N; ++j) {
-      w = ld64(B, col[j] + g8);
       const us2 J = {(unsigned short)j, (unsigned short)j};
-      lo = __builtin_elementwise_min(lo, as_us2(w.x) | J);
-      hi = __builtin_elementwise_min(hi, as_us2(w.y) | J);
+      lo = __builtin_elementwise_min(lo, as_us2(w[j].x) | J);
+      hi = __builtin_elementwise_min(hi, as_us2(w[j].y) | J);
     }
-    const uint32_t L = as_u32(lo), H = as_u32(hi);
-    // qtab sits at LDS offset 0, so qlane < 2^QSH and the member plane offset
-    // can be OR-ed in: (x << 10 & 0x3C00) | qlane -> v_lshlrev + v_and_or_b32
+  };
+  // stage 3a: the nearest members' quorum latencies (qtab sits at LDS offset
+  // 0, so qlane < 2^QSH and the member plane offset can be OR-ed in)
+  auto qread = [&](us2 lo, us2 hi, uint32_t (&q)[NQ]) {
     constexpr uint32_t QM = 15u << QSH;
-    const uint32_t q0 = ld32(B, ((L << QSH) & QM) | qlane);
-    const uint32_t q1 = ld32(B, ((L >> (16 - QSH)) & QM) | qlane);
-    const uint32_t q2 = ld32(B, ((H << QSH) & QM) | qlane);
-    const uint32_t q3 = ld32(B, ((H >> (16 - QSH)) & QM) | qlane);
-    const us2 dlo = lo >> (us2)4, dhi = hi >> (us2)4;
-    {
-      us2 a01 = dlo + as_us2(__builtin_amdgcn_perm(q1, q0, 0x05040100u));
-      us2 a23 = dhi + as_us2(__builtin_amdgcn_perm(q3, q2, 0x05040100u));
-      a01 = as_us2(as_u32(a01) & mlo);
-      a23 = as_us2(as_u32(a23) & mhi);
-      S1[0] = __builtin_amdgcn_udot2(a01, ones, S1[0], false);
-      S1[0] = __builtin_amdgcn_udot2(a23, ones, S1[0], false);
-      s2[0] = __builtin_amdgcn_udot2(a01, a01, s2[0], false);
-      s2[0] = __builtin_amdgcn_udot2(a23, a23, s2[0], false);
-    }
-    if (NL >= 2) {
-      us2 a01 = dlo + as_us2(__builtin_amdgcn_perm(q1, q0, 0x07060302u));
-      us2 a23 = dhi + as_us2(__builtin_amdgcn_perm(q3, q2, 0x07060302u));
-      a01 = as_us2(as_u32(a01) & mlo);
-      a23 = as_us2(as_u32(a23) & mhi);
-      S1[NL >= 2 ? 1 : 0] = __builtin_amdgcn_udot2(a01, ones, S1[NL >= 2 ? 1 : 0], false);
-      S1[NL >= 2 ? 1 : 0] = __builtin_amdgcn_udot2(a23, ones, S1[NL >= 2 ? 1 : 0], false);
-      s2[NL >= 2 ? 1 : 0] = __builtin_amdgcn_udot2(a01, a01, s2[NL >= 2 ? 1 : 0], false);
-      s2[NL >= 2 ? 1 : 0] = __builtin_amdgcn_udot2(a23, a23, s2[NL >= 2 ? 1 : 0], false);
-    }
+    const uint32_t L = as_u32(lo), H = as_u32(hi);
+    q[0] = ld32(B, ((L << QSH) & QM) | qlane);
+    q[1] = ld32(B, ((L >> (16 - QSH)) & QM) | qlane);
+    q[2] = ld32(B, ((H << QSH) & QM) | qlane);
+    q[3] = ld32(B, ((H >> (16 - QSH)) & QM) | qlane);
     if (NL == 3) {
       const uint32_t P2 = (uint32_t)N << QSH;  // second plane follows the first
-      const uint32_t r0 = ld32(B, qlane + P2 + ((L & 15u) << QSH));
-      const uint32_t r1 = ld32(B, qlane + P2 + (((L >> 16) & 15u) << QSH));
-      const uint32_t r2 = ld32(B, qlane + P2 + ((H & 15u) << QSH));
-      const uint32_t r3 = ld32(B, qlane + P2 + (((H >> 16) & 15u) << QSH));
-      us2 a01 = dlo + as_us2(__builtin_amdgcn_perm(r1, r0, 0x05040100u));
-      us2 a23 = dhi + as_us2(__builtin_amdgcn_perm(r3, r2, 0x05040100u));
-      a01 = as_us2(as_u32(a01) & mlo);
-      a23 = as_us2(as_u32(a23) & mhi);
-      S1[NL - 1] = __builtin_amdgcn_udot2(a01, ones, S1[NL - 1], false);
-      S1[NL - 1] = __builtin_amdgcn_udot2(a23, ones, S1[NL - 1], false);
-      s2[NL - 1] = __builtin_amdgcn_udot2(a01, a01, s2[NL - 1], false);
-      s2[NL - 1] = __builtin_amdgcn_udot2(a23, a23, s2[NL - 1], false);
+      q[NQ - 4] = ld32(B, qlane + P2 + ((L & 15u) << QSH));
+      q[NQ - 3] = ld32(B, qlane + P2 + (((L >> 16) & 15u) << QSH));
+      q[NQ - 2] = ld32(B, qlane + P2 + ((H & 15u) << QSH));
+      q[NQ - 1] = ld32(B, qlane + P2 + (((H >> 16) & 15u) << QSH));
     }
+  };
+  // stage 3b: client latency = distance + quorum latency; S1 and S2 by dot2
+  auto acc1 = [&](int t, us2 dlo, us2 dhi, uint32_t ql01, uint32_t ql23, uint32_t mlo, uint32_t mhi) {
+    us2 a01 = dlo + as_us2(ql01), a23 = dhi + as_us2(ql23);
+    a01 = as_us2(as_u32(a01) & mlo);
+    a23 = as_us2(as_u32(a23) & mhi);
+    S1[t] = __builtin_amdgcn_udot2(a01, ones, S1[t], false);
+    S1[t] = __builtin_amdgcn_udot2(a23, ones, S1[t], false);
+    s2[t] = __builtin_amdgcn_udot2(a01, a01, s2[t], false);
+    s2[t] = __builtin_amdgcn_udot2(a23, a23, s2[t], false);
+  };
+  auto accum = [&](us2 lo, us2 hi, const uint32_t (&q)[NQ], uint32_t mlo, uint32_t mhi) {
+    const us2 dlo = lo >> (us2)4, dhi = hi >> (us2)4;
+    acc1(0, dlo, dhi, __builtin_amdgcn_perm(q[1], q[0], 0x05040100u), __builtin_amdgcn_perm(q[3], q[2], 0x05040100u),
+         mlo, mhi);
+    if (NL >= 2)
+      acc1(NL >= 2 ? 1 : 0, dlo, dhi, __builtin_amdgcn_perm(q[1], q[0], 0x07060302u),
+           __builtin_amdgcn_perm(q[3], q[2], 0x07060302u), mlo, mhi);
+    if (NL == 3)
+      acc1(NL - 1, dlo, dhi, __builtin_amdgcn_perm(q[NQ - 3], q[NQ - 4], 0x05040100u),
+           __builtin_amdgcn_perm(q[NQ - 1], q[NQ - 2], 0x05040100u), mlo, mhi);
+  };
+  auto quad = [&](uint32_t g8, uint32_t mlo, uint32_t mhi) {
+    uint2 w[N];
+    uint32_t q[NQ];
+    us2 lo, hi;
+    load(g8, w);
+    nearest(w, lo, hi);
+    qread(lo, hi, q);
+    accum(lo, hi, q, mlo, mhi);
   };
   auto flush = [&]() {
 #pragma unroll
@@ -176,16 +189,45 @@ __device__ __forceinline__ void client_quads(const unsigned char* B, uint32_t cq
     }
   };
 
-  for (uint32_t g0 = 0; g0 < nq; g0 += flushQ) {
-    const uint32_t ge = min(nq, g0 + flushQ);
-    uint32_t g = g0;
-    for (; g + 4 <= ge; g += 4) {
-      quad(g * 8 + 0, ~0u, ~0u);
-      quad(g * 8 + 8, ~0u, ~0u);
-      quad(g * 8 + 16, ~0u, ~0u);
-      quad(g * 8 + 24, ~0u, ~0u);
+  uint32_t g = 0;
+  if (N <= 8 && flushQ >= 2) {
+    // Software-pipelined pairs: the next pair's 2N column reads (merged
+    // into ds_read2_b64) are in flight while this pair's qtab reads and
+    // sums run; the scheduling barriers keep the compiler from serialising
+    // the reads behind their first use, which it otherwise does to save
+    // registers under the 128-VGPR cap.
+    const uint32_t np = nq >> 1;
+    const uint32_t fp = flushQ >> 1;
+    if (np) {
+      uint2 wa[N], wb[N];
+      load(0, wa);
+      load(8, wb);
+      uint32_t k = 0;
+      for (uint32_t p = 0; p < np; ++p) {
+        us2 loA, hiA, loB, hiB;
+        nearest(wa, loA, hiA);
+        nearest(wb, loB, hiB);
+        uint32_t qA[NQ], qB[NQ];
+        qread(loA, hiA, qA);
+        qread(loB, hiB, qB);
+        const uint32_t gn = min(p + 1, np - 1) * 16;
+        load(gn, wa);
+        load(gn + 8, wb);
+        __builtin_amdgcn_sched_barrier(0);
+        accum(loA, hiA, qA, ~0u, ~0u);
+        accum(loB, hiB, qB, ~0u, ~0u);
+        if (++k == fp) {
+          flush();
+          k = 0;
+        }
+      }
+      flush();
+      g = np << 1;
     }
-    for (; g < ge; ++g) quad(g * 8, ~0u, ~0u);
+  }
+  for (uint32_t g0 = g; g0 < nq; g0 += flushQ) {
+    const uint32_t ge = min(nq, g0 + flushQ);
+    for (g = g0; g < ge; ++g) quad(g * 8, ~0u, ~0u);
     flush();
   }
   if (rem) {
@@ -302,9 +344,15 @@ __global__ void __launch_bounds__(FAST_BD, 4) sweep_fast_kernel(FastArgs a) {
         for (int j = 0; j < N; ++j) {
           uint32_t v[P];
           int t = 0;
+          if (a.ablate & 2) {
 #pragma unroll
-          for (int k = 0; k < N; ++k)
-            if (k != j) v[t++] = ld16(B, colR[k] + rowq[j]) >> LAT_SHIFT;
+            for (int k = 0; k < N; ++k)
+              if (k != j) v[t++] = colR[k] + rowq[j] + k;
+          } else {
+#pragma unroll
+            for (int k = 0; k < N; ++k)
+              if (k != j) v[t++] = ld16(B, colR[k] + rowq[j]) >> LAT_SHIFT;
+          }
 #pragma unroll
           for (int k = N - 1; k < P; ++k) v[k] = 0xFFFFFFFFu;
           sort_network<P>(v);
@@ -320,13 +368,17 @@ __global__ void __launch_bounds__(FAST_BD, 4) sweep_fast_kernel(FastArgs a) {
           }
           *(uint32_t*)(smem + qlane + ((uint32_t)j << QSH)) = ql[0] | (NL >= 2 ? ql[NL >= 2 ? 1 : 0] << 16 : 0u);
           if (NL == 3) *(uint32_t*)(smem + qlane + ((uint32_t)(N + j) << QSH)) = ql[NL - 1];
+#if BOTE_QROW_BARRIER
           // one member row at a time: keeps the row's reads and sort network
           // from being interleaved with the next rows (register pressure)
           __builtin_amdgcn_sched_barrier(0);
+#endif
         }
         // ---- FPaxos leader (f = 1, q = 2, min COV, first in config order)
         uint32_t bi = 0;
         bool amb = false;
+        // the leader's position, quorum latencies and column, carried along
+        uint32_t lp = p[0], lq2 = Q2[0], lq3 = Q3[0], lcol = colR[0];
         {
           uint32_t c1 = s.cs1[p[0]];
           double bS = (double)(c1 + nc * Q2[0]);
@@ -345,6 +397,10 @@ __global__ void __launch_bounds__(FAST_BD, 4) sweep_fast_kernel(FastArgs a) {
               bi = l;
               bS = S;
               bV = V;
+              lp = p[l];
+              lq2 = Q2[l];
+              lq3 = Q3[l];
+              lcol = colR[l];
             }
           }
         }
@@ -355,14 +411,20 @@ __global__ void __launch_bounds__(FAST_BD, 4) sweep_fast_kernel(FastArgs a) {
           have = false;
         }
         if (have) {
-          const uint32_t lp = sel_u(p, bi), lq2 = sel_u(Q2, bi), lq3 = sel_u(Q3, bi);
-          const uint32_t lcol = sel_u(colR, bi);
           Mom mom[NSLOT];
           // Input leaderless: the hot loop (first, so little is live across it)
           {
             uint32_t S1[NL];
             uint64_t S2[NL];
-            client_quads<N, NL>(B, s.cqt, nq, rem, a.s2_flush, colT, qlane, S1, S2);
+            client_quads<N, NL>(B, s.cqt, (a.ablate & 1) ? 0u : nq, (a.ablate & 1) ? 0u : rem, a.s2_flush, colT,
+                                qlane, S1, S2);
+            if (a.ablate & 1) {  // timing only: non-degenerate dummy sums (nothing defers)
+#pragma unroll
+              for (int t = 0; t < NL; ++t) {
+                S1[t] = 1000u + colT[0] + t;
+                S2[t] = (uint64_t)S1[t] * S1[t] + 12345u;
+              }
+            }
             mom[SLOT_AF1] = Mom{S1[QC::idx_a1], S2[QC::idx_a1], nc};
             mom[SLOT_AF2] = Mom{S1[QC::idx_a2], S2[QC::idx_a2], nc};
             mom[SLOT_E] = Mom{S1[QC::idx_e], S2[QC::idx_e], nc};
@@ -396,10 +458,9 @@ __global__ void __launch_bounds__(FAST_BD, 4) sweep_fast_kernel(FastArgs a) {
           }
           // ---- compute_score validity and score (search.rs:421-472)
           bool valid = false;
-          double score = 0.0;
-          if (a.want_score) {
+          const int fcap = min(N / 2, a.ft_metric);
+          if (a.want_score && !(a.ablate & 8)) {
             valid = true;
-            const int fcap = min(N / 2, a.ft_metric);
 #pragma unroll
             for (int f = 1; f <= 2; ++f) {
               if (f > fcap) break;
@@ -431,19 +492,6 @@ __global__ void __launch_bounds__(FAST_BD, 4) sweep_fast_kernel(FastArgs a) {
                 valid = valid && eok;
               }
             }
-            if (valid && !amb) {
-              const double me = mom_mean(mom[SLOT_E]);
-#pragma unroll
-              for (int f = 1; f <= 2; ++f) {
-                if (f > fcap) break;
-                const double mA = mom_mean(mom[f == 1 ? SLOT_AF1 : SLOT_AF2]);
-                const double fmi = mom_mean(mom[f == 1 ? SLOT_FF1 : SLOT_FF2]) - mA;
-                const double emi = me - mA;
-                double t = 30.0 * emi;
-                t = fmi + t;
-                score = score + t;
-              }
-            }
           }
           if (amb) {
             unsigned long long q = atomicAdd(a.queue_count, 1ull);
@@ -451,7 +499,7 @@ __global__ void __launch_bounds__(FAST_BD, 4) sweep_fast_kernel(FastArgs a) {
             have = false;
           } else {
             if (valid) ++valid_cnt;
-            if (a.want_digest) {
+            if (a.want_digest && !(a.ablate & 16)) {
               uint32_t h = 0;
 #pragma unroll
               for (int sl = 0; sl < NSLOT; ++sl)
@@ -465,8 +513,41 @@ __global__ void __launch_bounds__(FAST_BD, 4) sweep_fast_kernel(FastArgs a) {
               if (o >= a.n_obj) break;
               const uint32_t kind = a.obj_kind[o], sl = a.obj_slot[o];
               if (kind == OBJ_SCORE) {
-                ok[o] = valid;
-                key[o] = ~orderable_f64(score);
+                if (!valid) continue;
+                // score * nc = sum_f (S1_ff - S1_af) + 30 (S1_e - S1_af) exactly;
+                // the f64 score (search.rs:445-468) is within 1e-9 of it, so it
+                // is computed only when it may beat the objective's threshold.
+                const Rec th = s.tk.thr[o];
+                bool maybe = th.key == ~0ull;
+                if (!maybe) {
+                  const uint64_t ob = ~th.key;  // orderable bits of the threshold score
+                  const uint64_t bits = (ob >> 63) ? (ob & 0x7FFFFFFFFFFFFFFFull) : ~ob;
+                  const double tscore = __longlong_as_double((long long)bits);
+                  int64_t T = 0;
+#pragma unroll
+                  for (int f = 1; f <= 2; ++f) {
+                    if (f > fcap) break;
+                    const int64_t a1 = (int64_t)mom[f == 1 ? SLOT_AF1 : SLOT_AF2].s1;
+                    T += (int64_t)mom[f == 1 ? SLOT_FF1 : SLOT_FF2].s1 - a1 + 30 * ((int64_t)mom[SLOT_E].s1 - a1);
+                  }
+                  maybe = !(tscore == tscore) || (double)T >= (tscore - 1e-6) * (double)nc;
+                }
+                if (maybe) {
+                  double score = 0.0;
+                  const double me = mom_mean(mom[SLOT_E]);
+#pragma unroll
+                  for (int f = 1; f <= 2; ++f) {
+                    if (f > fcap) break;
+                    const double mA = mom_mean(mom[f == 1 ? SLOT_AF1 : SLOT_AF2]);
+                    const double fmi = mom_mean(mom[f == 1 ? SLOT_FF1 : SLOT_FF2]) - mA;
+                    const double emi = me - mA;
+                    double t = 30.0 * emi;
+                    t = fmi + t;
+                    score = score + t;
+                  }
+                  ok[o] = true;
+                  key[o] = ~orderable_f64(score);
+                }
                 continue;
               }
 #pragma unroll
@@ -491,7 +572,7 @@ __global__ void __launch_bounds__(FAST_BD, 4) sweep_fast_kernel(FastArgs a) {
           }
         }
       }
-      topk_step(s.tk, a.n_obj, a.K, key, ok, rank);
+      if (!(a.ablate & 4)) topk_step(s.tk, a.n_obj, a.K, key, ok, rank);
       if (jobok && rank < a.re) colex_next<N>(a.ns, p);
       ++rank;
     }
