@@ -3,6 +3,10 @@ shards, per-GPU top-K on the device, one all-gather of the fixed-size result
 blocks (RCCL over xGMI with backend "nccl"; gloo on CPU for tests) and a
 deterministic merge.  The merge order is by (key, rank), so the result does not
 depend on the number of shards (tests/test_dist.py, tests/test_gpu_parity.py).
+
+Reference: the only parallelism of the reference search is a rayon fork-join
+over client sets (fantoch_bote/src/search.rs:209-231); the rank-space split is
+this build's replacement.
 """
 from __future__ import annotations
 
@@ -11,27 +15,43 @@ from typing import Tuple
 
 def shard_range(total: int, world: int, rank: int) -> Tuple[int, int]:
     """Contiguous, balanced split of [0, total) (per-config cost is constant)."""
+    if world < 1 or not 0 <= rank < world:
+        raise ValueError(f"bad shard {rank} of {world}")
     return total * rank // world, total * (rank + 1) // world
 
 
-def sharded_sweep(sweep, stream=None, group=None):
+def sharded_sweep(sweep, stream=None, group=None, device: str = "cuda"):
     """Run `sweep` (fantoch_amd.bote.Sweep) over this rank's shard and return
-    the merged result of all ranks (every rank gets the same result)."""
+    the merged result of all ranks (every rank gets the same result).
+
+    `sweep` provides launch(rb, re, stream), result_bytes(),
+    result_device(ptr, stream), merge_device(src_ptr, n, dst_ptr, stream) and
+    parse_block(np.ndarray); the blocks live on `device`."""
     import torch
     import torch.distributed as dist
 
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     rank = dist.get_rank(group) if dist.is_initialized() else 0
     b, e = shard_range(sweep.total, world, rank)
-    st = stream if stream is not None else torch.cuda.current_stream().cuda_stream
-    sweep.launch(b, e, st)
+    if stream is None and device == "cuda":
+        stream = torch.cuda.current_stream().cuda_stream
+    sweep.launch(b, e, stream)
     nbytes = sweep.result_bytes()
-    blk = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
-    sweep.result_device(blk.data_ptr(), st)
+    blk = torch.empty(nbytes, dtype=torch.uint8, device=device)
+    sweep.result_device(blk.data_ptr(), stream)
     if world == 1:
         return sweep.parse_block(blk.cpu().numpy())
-    gathered = torch.empty(world * nbytes, dtype=torch.uint8, device="cuda")
+    gathered = torch.empty(world * nbytes, dtype=torch.uint8, device=device)
     dist.all_gather_into_tensor(gathered, blk, group=group)
-    out = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
-    sweep.merge_device(gathered.data_ptr(), world, out.data_ptr(), st)
+    out = torch.empty(nbytes, dtype=torch.uint8, device=device)
+    # merge_device takes at most 8 blocks per call: a tree for larger worlds
+    src, n = gathered, world
+    while n > 8:
+        groups = (n + 7) // 8
+        nxt = torch.empty(groups * nbytes, dtype=torch.uint8, device=device)
+        for g in range(groups):
+            k = min(8, n - 8 * g)
+            sweep.merge_device(src.data_ptr() + 8 * g * nbytes, k, nxt.data_ptr() + g * nbytes, stream)
+        src, n = nxt, groups
+    sweep.merge_device(src.data_ptr(), n, out.data_ptr(), stream)
     return sweep.parse_block(out.cpu().numpy())

@@ -1,0 +1,104 @@
+//! `Bote` / `Search` entry points over libbote_hip.so, keeping the reference
+//! signatures (fantoch_bote/src/lib.rs:38-121, search.rs:262-319).  Sketch for
+//! maintainers; not compiled here (no cargo in the image).
+use crate::hip;
+use fantoch::metrics::Histogram;
+use fantoch::planet::{Planet, Region};
+use fantoch_bote::protocol::{ClientPlacement, Protocol, ProtocolStats};
+
+/// A planet resident on one GPU.  Region ids are ranks of the region names,
+/// so the device's (latency, id) order is the reference's (latency, Region)
+/// order (fantoch/src/planet/mod.rs:122-140).
+pub struct HipBote {
+    dev: *mut hip::bote_planet,
+    names: Vec<Region>, // sorted by name; index == id
+}
+
+impl HipBote {
+    pub fn from(planet: &Planet, device: i32) -> Self {
+        let mut names: Vec<Region> = planet.regions().into_iter().cloned().collect();
+        names.sort();
+        let r = names.len();
+        let mut lat = vec![0u16; r * r];
+        for (i, a) in names.iter().enumerate() {
+            for (j, b) in names.iter().enumerate() {
+                lat[i * r + j] = planet.ping_latency(a, b).expect("latency") as u16;
+            }
+        }
+        let mut dev = std::ptr::null_mut();
+        hip::check(unsafe { hip::bote_planet_create(lat.as_ptr(), r as u32, device, &mut dev) });
+        HipBote { dev, names }
+    }
+
+    fn ids(&self, regions: &[Region]) -> Vec<u32> {
+        regions
+            .iter()
+            .map(|x| self.names.binary_search(x).expect("region in planet") as u32)
+            .collect()
+    }
+
+    /// Bote::leaderless (lib.rs:38-59)
+    pub fn leaderless<'a>(&self, servers: &[Region], clients: &'a [Region], quorum_size: usize) -> Vec<(&'a Region, u64)> {
+        let (s, c) = (self.ids(servers), self.ids(clients));
+        let mut out = vec![0u64; c.len()];
+        hip::check(unsafe {
+            hip::bote_leaderless(self.dev, s.as_ptr(), s.len() as u32, c.as_ptr(), c.len() as u32,
+                                 quorum_size as u32, out.as_mut_ptr())
+        });
+        clients.iter().zip(out).collect()
+    }
+
+    /// Bote::leader (lib.rs:67-89)
+    pub fn leader<'a>(&self, leader: &Region, servers: &[Region], clients: &'a [Region], quorum_size: usize)
+        -> Vec<(&'a Region, u64)> {
+        let (s, c) = (self.ids(servers), self.ids(clients));
+        let l = self.ids(std::slice::from_ref(leader))[0];
+        let mut out = vec![0u64; c.len()];
+        hip::check(unsafe {
+            hip::bote_leader(self.dev, l, s.as_ptr(), s.len() as u32, c.as_ptr(), c.len() as u32,
+                             quorum_size as u32, out.as_mut_ptr())
+        });
+        clients.iter().zip(out).collect()
+    }
+
+    /// Search::compute_stats (search.rs:262-319) for one configuration.
+    pub fn compute_stats(&self, config: &[Region], all_clients: &[Region]) -> ProtocolStats {
+        let (srv, cli) = (self.ids(config), self.ids(all_clients));
+        let (n, nc) = (srv.len(), cli.len());
+        let pos: Vec<u32> = (0..n as u32).collect();
+        let stride = 5 * nc + 5 * n;
+        let mut vals = vec![0u32; stride];
+        let null64 = std::ptr::null_mut();
+        hip::check(unsafe {
+            hip::bote_eval(self.dev, srv.as_ptr(), n as u32, cli.as_ptr(), nc as u32, n as u32, pos.as_ptr(), 0,
+                           1, std::ptr::null(), vals.as_mut_ptr(), std::ptr::null_mut(), null64, null64,
+                           std::ptr::null_mut(), std::ptr::null_mut(), std::ptr::null_mut(),
+                           std::ptr::null_mut())
+        });
+        // slot layout (include/bote_hip.h, bote_eval): af1 ff1 af2 ff2 e for
+        // Input (nc values each), then the same five for Colocated (n values)
+        let max_f = std::cmp::min(n / 2, 2);
+        let keys = [(Protocol::Atlas, 1), (Protocol::FPaxos, 1), (Protocol::Atlas, 2), (Protocol::FPaxos, 2),
+                    (Protocol::EPaxos, 0)];
+        let mut stats = ProtocolStats::new();
+        for (placement, base, len) in [(ClientPlacement::Input, 0, nc), (ClientPlacement::Colocated, 5 * nc, n)] {
+            for (k, (proto, f)) in keys.iter().enumerate() {
+                if *proto != Protocol::EPaxos && *f > max_f {
+                    continue;
+                }
+                let v = &vals[base + k * len..base + (k + 1) * len];
+                let hist = Histogram::from(v.iter().map(|x| *x as u64));
+                stats.insert(*proto, placement, *f, hist);
+            }
+        }
+        stats
+    }
+}
+
+impl Drop for HipBote {
+    fn drop(&mut self) {
+        unsafe {
+            hip::bote_planet_destroy(self.dev);
+        }
+    }
+}

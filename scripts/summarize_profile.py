@@ -1,0 +1,84 @@
+"""Summarise a scripts/gpu_profile.sh run (gpurun_out/prof/<TAG>_*) into
+profiles/<TAG>_profile.md and update profiles/traffic.json.
+
+  python scripts/summarize_profile.py r01 [workload_tag]
+
+Per kernel: calls and average duration (rocprofv3 --kernel-trace --stats), then
+the per-dispatch PMC averages of each counter pass.  HBM traffic per launch of
+the dominant kernel = FETCH_SIZE + WRITE_SIZE (rocprofv3 reports KiB).  The
+gfx950 FETCH_SIZE halving applies to 16-B/lane streaming reads only; this
+kernel's reads are a few KiB of staging loads, so the figure is used as is and
+marked uncalibrated (MI355X_MICROARCH.md "HBM").
+"""
+import collections
+import csv
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def main():
+    tag = sys.argv[1]
+    wl = sys.argv[2] if len(sys.argv) > 2 else "r64n7_n1"
+    src = os.path.join(ROOT, "gpurun_out", "prof")
+    out = []
+    stats = os.path.join(src, f"{tag}_trace", "run_kernel_stats.csv")
+    rows = list(csv.DictReader(open(stats)))
+    out.append(f"# rocprofv3 summary {tag} ({wl})\n")
+    out.append("## Kernel trace (`rocprofv3 --kernel-trace --stats`)\n")
+    out.append("| kernel | calls | avg ms | min ms | max ms | % |")
+    out.append("|---|---|---|---|---|---|")
+    dominant = None
+    for r in rows:
+        name = r["Name"]
+        out.append(f"| `{name[:70]}` | {r['Calls']} | {float(r['AverageNs']) / 1e6:.4f} | "
+                   f"{float(r['MinNs']) / 1e6:.4f} | {float(r['MaxNs']) / 1e6:.4f} | {float(r['Percentage']):.2f} |")
+        if dominant is None:
+            dominant = name
+    counters = collections.defaultdict(lambda: collections.defaultdict(float))
+    ndisp = collections.defaultdict(set)
+    i = 1
+    while os.path.exists(os.path.join(src, f"{tag}_pmc{i}", "run_counter_collection.csv")):
+        for r in csv.DictReader(open(os.path.join(src, f"{tag}_pmc{i}", "run_counter_collection.csv"))):
+            k = r["Kernel_Name"]
+            counters[k][r["Counter_Name"]] += float(r["Counter_Value"])
+            ndisp[(k, i)].add(r["Dispatch_Id"])
+            ndisp[(k, r["Counter_Name"])].add(r["Dispatch_Id"])
+        i += 1
+    out.append("\n## PMC per dispatch (separate `--pmc` passes, averaged over dispatches)\n")
+    traffic = None
+    for k, cs in counters.items():
+        if "sweep" not in k and "eval_kernel" not in k:
+            continue
+        out.append(f"### `{k[:80]}`\n")
+        out.append("| counter | per dispatch |")
+        out.append("|---|---|")
+        per = {}
+        for c, v in sorted(cs.items()):
+            per[c] = v / max(len(ndisp[(k, c)]), 1)
+            out.append(f"| {c} | {per[c]:.6g} |")
+        if "SQ_WAVE_CYCLES" in per and "SQ_WAIT_ANY" in per:
+            w = per["SQ_WAVE_CYCLES"]
+            out.append(f"\nwave-cycle split: active {per.get('SQ_ACTIVE_INST_ANY', 0) / w:.1%}, "
+                       f"wait (s_waitcnt/barrier) {per['SQ_WAIT_ANY'] / w:.1%}, "
+                       f"issue-stall {per.get('SQ_WAIT_INST_ANY', 0) / w:.1%}")
+        if "SQ_LDS_BANK_CONFLICT" in per and per.get("SQ_LDS_IDX_ACTIVE"):
+            out.append(f"LDS bank-conflict cycles / LDS active cycles: "
+                       f"{per['SQ_LDS_BANK_CONFLICT'] / per['SQ_LDS_IDX_ACTIVE']:.1%}")
+        if k == dominant and "FETCH_SIZE" in per and "WRITE_SIZE" in per:
+            traffic = (per["FETCH_SIZE"] + per["WRITE_SIZE"]) * 1024.0
+            out.append(f"HBM traffic per launch (FETCH_SIZE + WRITE_SIZE, KiB -> bytes): {traffic:.4g} B")
+        out.append("")
+    open(os.path.join(ROOT, "profiles", f"{tag}_profile.md"), "w").write("\n".join(out) + "\n")
+    if traffic is not None:
+        p = os.path.join(ROOT, "profiles", "traffic.json")
+        d = json.load(open(p)) if os.path.exists(p) else {}
+        d[wl] = traffic
+        json.dump(d, open(p, "w"), indent=1, sort_keys=True)
+    print("\n".join(out))
+
+
+if __name__ == "__main__":
+    main()

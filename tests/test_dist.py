@@ -1,0 +1,86 @@
+"""Multi-rank orchestration of the sharded sweep (fantoch_amd/dist.py) under
+gloo on CPU: world sizes 2, 3 and 9 (9 exercises the merge tree), each rank a
+separate process sweeping its contiguous rank shard through the oracle-backed
+stand-in (tests/oracle_sweep.py).  The merged top-K, valid count and digest
+must equal one unsharded sweep.  The GPU path (device blocks, RCCL) runs the
+same code with backend "nccl" in bench.py; tests/test_gpu_parity.py checks
+its device merge against shard-count independence."""
+import os
+import socket
+import sys
+
+import pytest
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+N, K = 5, 16
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _setup():
+    for p in (ROOT, os.path.join(ROOT, "oracle"), os.path.join(ROOT, "tests")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    import numpy as np
+
+    import oracle as O
+    from fantoch_amd.bote import DEFAULT_OBJECTIVES
+    from fantoch_amd.planet import Planet
+    from oracle_sweep import OracleSweep
+
+    p = Planet.new()
+    srv = np.arange(p.R, dtype=np.uint32)
+    return OracleSweep(O.OraclePlanet.of(p), srv, srv, N, DEFAULT_OBJECTIVES, K)
+
+
+def _worker(rank, world, port, q):
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from fantoch_amd.dist import sharded_sweep
+        sw = _setup()
+        res = sharded_sweep(sw, stream=None, device="cpu")
+        q.put((rank, res.tops, res.valid, res.digest))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3, 9])
+def test_sharded_sweep_gloo_equals_unsharded(world):
+    sw = _setup()
+    sw.launch(0, sw.total)
+    want = sw.parse_block(sw._blk)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=240) for _ in range(world)]
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    for rank, tops, valid, digest in got:
+        assert tops == want.tops, f"rank {rank}: merged top-K differs from the unsharded sweep"
+        assert (valid, digest) == (want.valid, want.digest)
+
+
+def test_shard_range_partition():
+    from fantoch_amd.dist import shard_range
+    for total in (0, 1, 7, 621216192, 5423611200):
+        for world in (1, 2, 3, 8):
+            rs = [shard_range(total, world, r) for r in range(world)]
+            assert rs[0][0] == 0 and rs[-1][1] == total
+            assert all(rs[i][1] == rs[i + 1][0] for i in range(world - 1))
+            assert max(e - b for b, e in rs) - min(e - b for b, e in rs) <= 1
+    with pytest.raises(ValueError):
+        shard_range(10, 2, 2)

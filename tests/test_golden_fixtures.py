@@ -1,0 +1,67 @@
+"""The committed fixtures (tests/golden/make_golden.py) against the planet
+loader and the CPU oracle.  CPU only; tests/test_gpu_parity.py checks the HIP
+path against the same files."""
+import json
+import os
+from math import comb
+
+import numpy as np
+import pytest
+
+import oracle as O
+from fantoch_amd.bote import DEFAULT_OBJECTIVES
+from fantoch_amd.planet import AWS_2020_DIR, AWS_2021_DIR, Planet
+
+G = os.path.join(os.path.dirname(__file__), "golden")
+RP = (110.0, 35.0, 0.0, 15.0)
+
+
+@pytest.fixture(scope="module")
+def stats():
+    return np.load(os.path.join(G, "gcp_n3_n5_stats.npz"))
+
+
+@pytest.fixture(scope="module")
+def topk():
+    return json.load(open(os.path.join(G, "topk.json")))
+
+
+def test_planets_fixture_matches_loader():
+    z = np.load(os.path.join(G, "planets.npz"))
+    for key, p in (("gcp", Planet.new()), ("aws20", Planet.from_dir(AWS_2020_DIR)),
+                   ("aws21", Planet.from_dir(AWS_2021_DIR))):
+        assert list(z[f"{key}_names"]) == p.names
+        assert np.array_equal(z[f"{key}_lat"], p.lat.astype(np.uint16))
+
+
+@pytest.mark.parametrize("n,step", [(3, 1), (5, 7)])
+def test_oracle_per_config_matches_fixture(stats, n, step):
+    p = Planet.new()
+    o = O.OraclePlanet.of(p)
+    srv = np.arange(p.R, dtype=np.uint32)
+    ranks = np.arange(0, comb(p.R, n), step)
+    cfg = np.array([O.colex_unrank(int(r), n, p.R) for r in ranks], dtype=np.uint32)
+    vals, lead = o.compute_stats(cfg, srv)
+    assert np.array_equal(lead, stats[f"n{n}_leader"][ranks])
+    nc = p.R
+    for slot in range(10):
+        if n < 4 and slot % 5 in (2, 3):
+            continue
+        v = vals[:, slot * nc:(slot + 1) * nc] if slot < 5 else vals[:, 5 * nc + (slot - 5) * n:5 * nc + (slot - 4) * n]
+        assert np.array_equal(v.sum(axis=1), stats[f"n{n}_s1"][ranks, slot].astype(np.uint64))
+        assert np.array_equal((v * v).sum(axis=1), stats[f"n{n}_s2"][ranks, slot])
+    sc, va = o.scores(cfg, srv, RP, 2)
+    assert np.array_equal(va, stats[f"n{n}_valid"][ranks])
+    assert np.array_equal(sc.view(np.uint64), stats[f"n{n}_score"][ranks].view(np.uint64))
+
+
+@pytest.mark.parametrize("case", ["gcp_n3", "gcp_n5", "gcp_n13", "aws21_n3", "aws21_n5"])
+def test_oracle_topk_matches_fixture(topk, case):
+    c = topk["cases"][case]
+    p = Planet.new() if case.startswith("gcp") else Planet.from_dir(AWS_2021_DIR)
+    o = O.OraclePlanet.of(p)
+    s = np.arange(p.R, dtype=np.uint32)
+    tops, valid, digest = o.sweep(s, s, c["n"], c["rank_begin"], c["rank_end"], DEFAULT_OBJECTIVES, topk["K"],
+                                  RP, 2, 4)
+    assert valid == c["valid"] and str(digest) == c["digest"]
+    assert [[[str(k), r] for k, r in t] for t in tops] == c["tops"]
