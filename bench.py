@@ -21,6 +21,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "region configs evaluated/sec (1/2/4/8 GPUs), synthetic 64-region planet n=7 f=1,2"
+KERNEL_NAMES = {"group": "sweep_group_kernel<N> (bote_group.hip)", "fast": "sweep_fast_kernel<N> (bote_sweep.hip)",
+                "generic": "eval_kernel<N,false> (bote_kernels.hip)"}
 VALU_PEAK_TOPS = 78.6  # 256 CU x 4 SIMD x 32 lanes x 2.4 GHz (MI355X_MICROARCH.md chip table)
 
 
@@ -161,12 +163,11 @@ def main():
             "config": {"workload": wl["desc"], "regions": planet.R, "n": n, "configs_per_step": total,
                        "keys": 10, "objectives": len(DEFAULT_OBJECTIVES), "K": 100,
                        "parallelism": f"rank-shard x{world}", "grid": grid, "block": block, "lds_bytes": lds,
-                       "kernel_path": "fast" if sweep.is_fast() else "generic"},
+                       "kernel_path": sweep.kernel_path()},
             "roofline": {"bound": "valu", "achieved": achieved, "peak": VALU_PEAK_TOPS, "unit": "Tops/s",
                          "frac": achieved / VALU_PEAK_TOPS, "traffic": traffic,
                          "work_per_config": W, "kernel_ms_avg": kavg_ms,
-                         "kernel": ("sweep_fast_kernel<N> (bote_sweep.hip)" if sweep.is_fast()
-                                    else "eval_kernel<N,false> (bote_kernels.hip)")},
+                         "kernel": KERNEL_NAMES[sweep.kernel_path()]},
             "result_check": {"valid": res.valid, "digest": res.digest,
                              "top_score_rank": res.tops[0][0][1] if res.tops[0] else None},
         }

@@ -513,9 +513,14 @@ class Sweep:
         return ms.value, n.value
 
     def is_fast(self) -> bool:
+        """True when a fast-path kernel (packed or group) runs the sweep."""
+        return self.kernel_path() != "generic"
+
+    def kernel_path(self) -> str:
+        """'generic' (bote_kernels.hip), 'fast' (bote_sweep.hip) or 'group' (bote_group.hip)."""
         v = C.c_int()
         check(lib().bote_sweep_is_fast(self.h, C.byref(v)))
-        return bool(v.value)
+        return ("generic", "fast", "group")[v.value]
 
     def geometry(self) -> Tuple[int, int, int]:
         g, b, l = C.c_uint32(), C.c_uint32(), C.c_uint32()

@@ -116,11 +116,13 @@ struct bote_sweep {
   bool launched = false;
   // fast path (bote_sweep.hip) + exact fixup of its deferred configs
   bool fast = false;
+  bool group = false;  // fast path runs the group kernel (bote_group.hip)
+  bool def_obj = false;  // the default objective set, compiled into the group kernel
   bote::FastArgs fargs{};
   uint32_t fgrid = 0;
   size_t fshm = 0;
   uint32_t xgrid = 0;  // generic fixup grid (deferred configs)
-  DBuf cqt, rqt, queue, qcount;
+  DBuf cqt, rqt, queue, qcount, lowtab;
   uint64_t last_rb = 0, last_re = 0;
   hipStream_t last_stream = nullptr;
   uint64_t result_bytes() const { return (uint64_t)n_obj * bote::KP * 16 + 16; }
@@ -154,6 +156,30 @@ std::vector<uint16_t> quad_layout(const bote_planet* p, const uint32_t* rows, ui
     for (uint32_t c = 0; c < nrows; ++c)
       m[(size_t)t * stride + c] = (uint16_t)(p->lat[(size_t)rows[c] * p->R + t] << bote::LAT_SHIFT);
   return m;
+}
+// Expected lane utilisation of the group kernel over the whole rank space:
+// groups with smallest fixed position k hold C(k, 3) configs and run in
+// ceil(C(k, 3) / 64) wavefront steps (bote_group.hip).
+double group_utilisation(uint32_t ns, uint32_t n) {
+  const uint32_t F = n - 3;
+  long double cfg = 0, steps = 0;
+  for (uint32_t k = 3; k + F <= ns; ++k) {
+    const long double groups = (long double)binom_u64(ns - 1 - k, F - 1);
+    const uint64_t g = binom_u64(k, 3);
+    cfg += groups * g;
+    steps += groups * (long double)((g + 63) / 64);
+  }
+  return steps > 0 ? (double)(cfg / (64 * steps)) : 0.0;
+}
+
+// Packed (p0 | p1 << 8 | p2 << 16) 3-subsets of [0, m) in colex order.
+std::vector<uint32_t> low_table(uint32_t m) {
+  std::vector<uint32_t> t;
+  t.reserve(binom_u64(m, 3));
+  for (uint32_t p2 = 2; p2 < m; ++p2)
+    for (uint32_t p1 = 1; p1 < p2; ++p1)
+      for (uint32_t p0 = 0; p0 < p1; ++p0) t.push_back(p0 | (p1 << 8) | (p2 << 16));
+  return t;
 }
 }  // namespace
 
@@ -523,7 +549,11 @@ int bote_sweep_create(const bote_planet* p, const uint32_t* servers, uint32_t ns
   s->xgrid = 32;
 
   // ---- fast path: quad layouts, column sums are computed on the device
-  s->fast = fast_eligible(p, servers, ns, nc, has_score ? rp : nullptr) && !getenv("BOTE_FORCE_GENERIC");
+  // BOTE_SWEEP_KERNEL=generic|fast|group forces a path (tests, A/B timing);
+  // by default: group kernel when eligible and >= 90 % lane utilisation.
+  const char* kern = getenv("BOTE_SWEEP_KERNEL");
+  const bool force_generic = getenv("BOTE_FORCE_GENERIC") || (kern && !strcmp(kern, "generic"));
+  s->fast = fast_eligible(p, servers, ns, nc, has_score ? rp : nullptr) && !force_generic;
   if (s->fast) {
     bote::FastArgs& f = s->fargs;
     f = bote::FastArgs{};
@@ -581,6 +611,29 @@ int bote_sweep_create(const bote_planet* p, const uint32_t* servers, uint32_t ns
     } else {
       s->fgrid = (uint32_t)(device_cus(p->device) * bote::fast_occupancy(n, s->fshm));
     }
+    // group kernel: n >= 4, positions fit 8 bits, enough lane utilisation
+    bool want_group = n >= 4 && ns <= 256 && group_utilisation(ns, n) >= 0.9;
+    if (kern) want_group = n >= 4 && ns <= 256 && !strcmp(kern, "group");
+    if (s->fast && want_group) {
+      auto lt = low_table(ns - (n - 3));
+      if (s->lowtab.alloc(std::max<size_t>(lt.size(), 1) * 4) != hipSuccess)
+        return cleanup(fail(BOTE_E_NOMEM, "hipMalloc group low table"));
+      if (!lt.empty() && hipMemcpy(s->lowtab.p, lt.data(), lt.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
+        return cleanup(fail(BOTE_E_DEVICE, "upload group low table"));
+      f.lowtab = s->lowtab.as<uint32_t>();
+      const size_t gshm = bote::group_smem_bytes(f, n);
+      // bote.py DEFAULT_OBJECTIVES: SCORE, MEAN af1, MEAN ff1, COV af1, MEAN e
+      static const uint32_t dk[5] = {BOTE_OBJ_SCORE, BOTE_OBJ_MEAN, BOTE_OBJ_MEAN, BOTE_OBJ_COV, BOTE_OBJ_MEAN};
+      static const uint32_t ds[5] = {0, BOTE_SLOT_AF1, BOTE_SLOT_FF1, BOTE_SLOT_AF1, BOTE_SLOT_E};
+      s->def_obj = n_obj == 5 && f.want_score && !getenv("BOTE_NO_DEF_OBJ");
+      for (uint32_t o = 0; s->def_obj && o < 5; ++o)
+        s->def_obj = objs[o].kind == dk[o] && (dk[o] == BOTE_OBJ_SCORE || objs[o].slot == ds[o]);
+      if (gshm <= device_max_lds(p->device)) {
+        s->group = true;
+        s->fshm = gshm;
+        s->fgrid = (uint32_t)(device_cus(p->device) * bote::group_occupancy(n, gshm, s->def_obj));
+      }
+    }
   }
   // the generic path may also run on a fast sweep (overflow recompute)
   const uint32_t lists = s->fast ? std::max(s->grid, s->fgrid + s->xgrid) : s->grid;
@@ -599,7 +652,7 @@ int bote_sweep_create(const bote_planet* p, const uint32_t* servers, uint32_t ns
 
 int bote_sweep_is_fast(const bote_sweep* s, int* out) {
   if (!s || !out) return fail(BOTE_E_ARG, "null argument");
-  *out = s->fast ? 1 : 0;
+  *out = s->fast ? (s->group ? 2 : 1) : 0;
   return BOTE_OK;
 }
 
@@ -671,7 +724,8 @@ static int launch_fast_path(bote_sweep* s, uint64_t rb, uint64_t re, hipStream_t
   if ((rc = timing_slot(s, e0, e1))) return rc;
   HIP_TRY(hipEventRecord(s->ev0, st));
   HIP_TRY(hipEventRecord(*e0, st));
-  HIP_TRY(bote::launch_fast(f, s->n, s->fgrid, s->fshm, st));
+  if (s->group) HIP_TRY(bote::launch_group(f, s->n, s->def_obj, s->fgrid, s->fshm, st));
+  else HIP_TRY(bote::launch_fast(f, s->n, s->fgrid, s->fshm, st));
   HIP_TRY(hipEventRecord(*e1, st));
   HIP_TRY(hipEventRecord(s->ev1, st));
   // exact fixup of the deferred configs: generic kernel over the rank list

@@ -1,0 +1,810 @@
+// bote_group.hip — the group-structured sweep kernel (gfx950), the hot path
+// for fast-path planets with config size N >= 4.
+//
+// Colex ranks of n-subsets are grouped by their N-3 LARGEST members: every
+// rank sum_j C(p_j, j+1) with the same (p_3 .. p_{N-1}) lies in one contiguous
+// range of C(p_3, 3) ranks (a "group"), and inside it only (p_0, p_1, p_2)
+// vary.  A wavefront walks its contiguous share of the rank space group by
+// group, 64 configs (one per lane) at a time.  Everything that depends only on
+// the fixed members is computed once per group and is wave-uniform, kept in a
+// per-wave LDS line (broadcast reads, no SGPR pressure):
+//   * each client's nearest fixed member (packed latency << 4 | member), so
+//     the hot loop reads 3 lane columns + 1 broadcast line instead of N
+//     columns;
+//   * the fixed members' sorted distances to each other, packed two rows per
+//     word, so a fixed member's quorum latencies need only the 3 lane members
+//     inserted (v_pk_min_u16 / v_pk_max_u16 on two rows at once);
+//   * the fixed members' column statistics.
+// Per lane: the 3 variable rows are sorted in full (two of them packed), the
+// fixed rows get 3 insertions each, then leader selection, moments, validity,
+// digest and objective keys.  COV decisions are screened in f32 and fall back
+// to f64, then to deferral (the exact generic kernel), only inside their
+// ambiguity bands.
+//
+// The block top-K is merged wave by wave under an LDS lock (no block
+// barriers in the sweep): a wave whose configs may enter a list (key <= the
+// list's K-th key, read lock-free) takes the lock and merges exactly.
+//
+// LDS is addressed with absolute 32-bit addresses (lds_* helpers) so that the
+// per-client address arithmetic is one shift-add and constant offsets fold
+// into the ds_read offset fields.
+//
+// Reference map: see bote_kernels.hip's header (Search::compute_stats,
+// search.rs:262-319, and the Bote functions it calls, lib.rs:38-185).
+#include "bote_fast.hpp"
+
+#define AS3 __attribute__((address_space(3)))
+
+namespace bote {
+
+constexpr int WPB = FAST_BD / 64;  // wavefronts per workgroup
+constexpr uint32_t GQSH = 10;      // log2(FAST_BD * 4): byte stride between qtab member planes
+static_assert((1u << GQSH) == FAST_BD * 4, "qtab plane stride");
+
+__host__ __device__ constexpr int cmax(int a, int b) { return a > b ? a : b; }
+
+template <int N>
+struct GCfg {
+  using QC = QCfg<N>;
+  static constexpr int F = N - 3;         // wave-uniform (fixed) members
+  static constexpr int FP = (F + 1) / 2;  // fixed rows, packed in pairs
+  // a row's smallest off-diagonal distances that any quorum reads (ranks 0 .. KQ-1)
+  static constexpr int KQ = cmax(cmax(QC::qa1, QC::maxf >= 2 ? QC::qa2 : 0), cmax(QC::qe, 3)) - 1;
+  static_assert(KQ <= N - 1, "quorum larger than the config");
+};
+
+// per-wave group line: [mF: cq_quads+1 uint2][Upk: FP*KQ u32][fS1: F u32][fV: F f32]
+__host__ __device__ inline uint32_t gline_bytes(const FastArgs& a, int N, int KQ) {
+  const int F = N - 3, FP = (F + 1) / 2;
+  return (a.cq_quads + 1) * 8 + (uint32_t)(FP * KQ + 2 * F) * 4;
+}
+
+__host__ __device__ inline size_t group_layout(const FastArgs& a, int N, int NLW, int KQ, size_t* off) {
+  size_t o = 0;
+  off[0] = o; o += (size_t)N * FAST_BD * NLW * 4;  // qtab first: offsets stay small
+  off[1] = o; o += (size_t)a.R * (a.cq_quads + 1) * 8;
+  off[2] = o; o += a.rq_separate ? (size_t)a.R * (a.rq_quads + 1) * 8 : 0;
+  off[3] = o; o += (size_t)a.ns * 4;  // srv
+  off[4] = o; o += (size_t)a.ns * 4;  // cs1
+  o = (o + 15) & ~(size_t)15;
+  off[5] = o; o += (size_t)a.ns * 8;                   // cs2
+  off[6] = o; o += (size_t)a.ns * 8;                   // vcol (f64)
+  off[7] = o; o += (size_t)(a.ns + 1) * (N + 1) * 8;  // binom
+  off[8] = o; o += (size_t)WPB * gline_bytes(a, N, KQ);  // per-wave group lines
+  o = (o + 15) & ~(size_t)15;
+  off[9] = o; o += (size_t)a.n_obj * KP * 16;  // top
+  off[10] = o; o += (size_t)64 * 16;          // cand (one wave's candidates)
+  off[11] = o; o += (size_t)KP * 16;          // tmp
+  off[12] = o; o += (size_t)MAXOBJ * 16;      // thr
+  off[13] = o; o += 48;                       // lock
+  return o;
+}
+
+template <int N>
+static size_t group_smem_n(const FastArgs& a) {
+  size_t off[14];
+  return group_layout(a, N, QCfg<N>::NL <= 2 ? 1 : 2, GCfg<N>::KQ, off);
+}
+
+size_t group_smem_bytes(const FastArgs& a, uint32_t n) {
+  switch (n) {
+#define SM_CASE(NN) case NN: return group_smem_n<NN>(a);
+    SM_CASE(4) SM_CASE(5) SM_CASE(6) SM_CASE(7) SM_CASE(8) SM_CASE(9) SM_CASE(10) SM_CASE(11) SM_CASE(12)
+    SM_CASE(13) SM_CASE(14) SM_CASE(15) SM_CASE(16)
+#undef SM_CASE
+    default: return 0;
+  }
+}
+
+__device__ __forceinline__ uint32_t uni(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
+__device__ __forceinline__ uint64_t uni64(uint64_t x) {
+  return ((uint64_t)uni((uint32_t)(x >> 32)) << 32) | uni((uint32_t)x);
+}
+
+// absolute-address LDS access
+__device__ __forceinline__ uint32_t lds_base(const void* p) { return (uint32_t)(uintptr_t)(const AS3 void*)p; }
+__device__ __forceinline__ uint32_t l16(uint32_t a) { return *(const AS3 uint16_t*)(uintptr_t)a; }
+__device__ __forceinline__ uint32_t l32(uint32_t a) { return *(const AS3 uint32_t*)(uintptr_t)a; }
+__device__ __forceinline__ uint2 l64(uint32_t a) {
+  const uint64_t v = *(const AS3 uint64_t*)(uintptr_t)a;
+  return make_uint2((uint32_t)v, (uint32_t)(v >> 32));
+}
+__device__ __forceinline__ float lf32(uint32_t a) { return *(const AS3 float*)(uintptr_t)a; }
+__device__ __forceinline__ void s16(uint32_t a, uint32_t v) { *(AS3 uint16_t*)(uintptr_t)a = (uint16_t)v; }
+__device__ __forceinline__ void s32(uint32_t a, uint32_t v) { *(AS3 uint32_t*)(uintptr_t)a = v; }
+
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+__device__ __forceinline__ us2 pk_min(us2 a, us2 b) { return __builtin_elementwise_min(a, b); }
+__device__ __forceinline__ us2 pk_max(us2 a, us2 b) { return __builtin_elementwise_max(a, b); }
+
+// Batcher odd-even merge sort over packed u16 pairs (two rows at once)
+template <int P>
+__device__ __forceinline__ void sort_network_pk(uint32_t* a) {
+#pragma unroll
+  for (int p = 1; p < P; p <<= 1) {
+#pragma unroll
+    for (int k = p; k >= 1; k >>= 1) {
+#pragma unroll
+      for (int j = k % p; j + k < P; j += 2 * k) {
+#pragma unroll
+        for (int i = 0; i < k; ++i) {
+          if (i + j + k < P && (i + j) / (2 * p) == (i + j + k) / (2 * p)) {
+            const us2 x = as_us2(a[i + j]), y = as_us2(a[i + j + k]);
+            a[i + j] = as_u32(pk_min(x, y));
+            a[i + j + k] = as_u32(pk_max(x, y));
+          }
+        }
+      }
+    }
+  }
+}
+
+// ------------------------------------------------ wave-level top-K merge --
+// Called by a whole wavefront (uniform branch).  Takes the block's LDS lock,
+// merges every lane record that beats its objective's K-th record (exact
+// (key, rank) order), updates the thresholds, releases the lock.
+__device__ __forceinline__ void wave_topk(const TopkLds& t, int* lock, int n_obj, uint32_t K,
+                                          const uint64_t (&key)[MAXOBJ], const bool (&ok)[MAXOBJ], uint64_t rank) {
+  const uint32_t lane = threadIdx.x & 63;
+  if (lane == 0) {
+    while (atomicCAS(lock, 0, 1) != 0) __builtin_amdgcn_s_sleep(2);
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+#pragma unroll
+  for (int o = 0; o < MAXOBJ; ++o) {
+    if (o >= n_obj) break;
+    Rec* top = t.top + o * KP;
+    const Rec th = top[K - 1];
+    const Rec mine = Rec{key[o], rank};
+    const bool p = ok[o] && rec_lt(mine, th);
+    const uint64_t m = __ballot(p);
+    if (m == 0) continue;
+    const int n = __popcll(m);
+    if (p) t.cand[__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0))] = mine;
+    wave_sync();
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int e = lane + 64 * h;
+      const Rec x = top[e];
+      int r = e;
+      for (int j = 0; j < n; ++j) r += rec_lt(t.cand[j], x);
+      if (r < KP) t.tmp[r] = x;
+    }
+    if ((int)lane < n) {
+      const Rec y = t.cand[lane];
+      int r = lower_bound_rec(top, KP, y);
+      for (int j = 0; j < n; ++j) r += rec_lt(t.cand[j], y);
+      if (r < KP) t.tmp[r] = y;
+    }
+    wave_sync();
+    top[lane] = t.tmp[lane];
+    top[lane + 64] = t.tmp[lane + 64];
+    wave_sync();
+    if (lane == 0) t.thr[o] = top[K - 1];
+    wave_sync();
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  if (lane == 0) atomicExch(lock, 0);
+}
+
+// -------------------------------------- exact-order COV comparisons -------
+// sign of V_x * S_y^2 - V_y * S_x^2 (cov_x^2 vs cov_y^2): -1 / +1, or 0 when
+// inside the ambiguity band.  f32 screen first (S exact below 2^24; V carries
+// one rounding, every product one more): decided outside a 2^-18 relative
+// band; else f64 from the exact V (dVx(), dVy()) with the 2^-32 band the
+// generic path uses.
+template <class FX, class FY>
+__device__ __forceinline__ int cov2_sign(float Vx, uint32_t Sx, float Vy, uint32_t Sy, const FX& dVx, const FY& dVy) {
+  const float fx = (float)Sx, fy = (float)Sy;
+  const float x = Vx * (fy * fy), y = Vy * (fx * fx);
+  const float d = x - y, tol = 0x1p-18f * fmaxf(x, y);
+  if (d < -tol) return -1;
+  if (d > tol) return 1;
+  const double sx = (double)Sx, sy = (double)Sy;
+  const double X = dVx() * (sy * sy), Y = dVy() * (sx * sx);
+  const double D = X - Y, T = 0x1p-32 * fmax(X, Y);
+  return D < -T ? -1 : (D > T ? 1 : 0);
+}
+
+// ---------------------------------------------------------- the kernel ----
+// DEF: the default objective set (bote.py DEFAULT_OBJECTIVES: SCORE, MEAN af1,
+// MEAN ff1, COV af1, MEAN e), compiled in; otherwise the objectives come from
+// the arguments (finish_config, bote_fast.hpp).
+template <int N, bool DEF>
+__global__ void __launch_bounds__(FAST_BD, 4) sweep_group_kernel(FastArgs a) {
+  using QC = QCfg<N>;
+  using GC = GCfg<N>;
+  constexpr int NL = QC::NL;
+  constexpr int NLW = NL <= 2 ? 1 : 2;
+  constexpr int F = GC::F;
+  constexpr int FP = GC::FP;
+  constexpr int KQ = GC::KQ;
+  constexpr int PV = Pow2<N - 1>::v;                 // variable row: N-1 values, padded
+  constexpr int PF = Pow2<F>::v;                     // fixed-to-fixed row: F values (self = INF), padded
+  extern __shared__ __align__(16) unsigned char smem[];
+  size_t off[14];
+  group_layout(a, N, NLW, KQ, off);
+  const uint32_t LB = lds_base(smem);
+  const uint32_t qtab = LB + (uint32_t)off[0];
+  const uint32_t cqt = LB + (uint32_t)off[1];
+  const uint32_t rqt = LB + (uint32_t)(a.rq_separate ? off[2] : off[1]);
+  uint32_t* srv = (uint32_t*)(smem + off[3]);
+  uint32_t* cs1 = (uint32_t*)(smem + off[4]);
+  uint64_t* cs2 = (uint64_t*)(smem + off[5]);
+  double* vcol = (double*)(smem + off[6]);
+  uint64_t* binom = (uint64_t*)(smem + off[7]);
+  TopkLds tk;
+  tk.top = (Rec*)(smem + off[9]);
+  tk.cand = (Rec*)(smem + off[10]);
+  tk.tmp = (Rec*)(smem + off[11]);
+  tk.thr = (Rec*)(smem + off[12]);
+  tk.cnt = nullptr;
+  int* lock = (int*)(smem + off[13]);
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+
+  // ---- stage: quad matrices, server list, binomials; then per-position sums
+  {
+    const uint32_t cw = a.R * (a.cq_quads + 1) * 2;
+    const uint32_t* src = (const uint32_t*)a.cqt;
+    uint32_t* dst = (uint32_t*)(smem + off[1]);
+    for (uint32_t i = tid; i < cw; i += FAST_BD) dst[i] = src[i];
+    if (a.rq_separate) {
+      const uint32_t rw = a.R * (a.rq_quads + 1) * 2;
+      const uint32_t* rs = (const uint32_t*)a.rqt;
+      uint32_t* rd = (uint32_t*)(smem + off[2]);
+      for (uint32_t i = tid; i < rw; i += FAST_BD) rd[i] = rs[i];
+    }
+  }
+  for (uint32_t i = tid; i < a.ns; i += FAST_BD) srv[i] = a.srv[i];
+  for (uint32_t i = tid; i < (a.ns + 1) * (N + 1); i += FAST_BD) binom[i] = a.binom[i];
+  for (uint32_t i = tid; i < (uint32_t)a.n_obj * KP; i += FAST_BD) tk.top[i] = rec_max();
+  if (tid < MAXOBJ) tk.thr[tid] = rec_max();
+  if (tid == 0) *lock = 0;
+  __syncthreads();
+  const uint32_t cstride = (a.cq_quads + 1) * 8;  // bytes per CQT column
+  const uint32_t rstride = (a.rq_quads + 1) * 8;
+  for (uint32_t i = tid; i < a.ns; i += FAST_BD) {
+    const uint32_t col = cqt + srv[i] * cstride;
+    uint64_t c1 = 0, c2 = 0;
+    for (uint32_t c = 0; c < a.nc; ++c) {
+      uint64_t v = l16(col + 2 * c) >> LAT_SHIFT;
+      c1 += v;
+      c2 += v * v;
+    }
+    cs1[i] = (uint32_t)c1;
+    cs2[i] = c2;
+    vcol[i] = (double)((uint64_t)a.nc * c2 - c1 * c1);  // exact: < 2^53
+  }
+  __syncthreads();
+
+  const uint32_t nc = a.nc, nq = nc >> 2, rem = nc & 3;
+  const uint32_t qlane = qtab + tid * 4;
+  const uint32_t gl = LB + (uint32_t)off[8] + wid * gline_bytes(a, N, KQ);  // this wave's group line
+  const uint32_t mfl = gl;                                                 // nearest fixed member per client
+  const uint32_t upk = gl + cstride;                                       // packed fixed-row lists
+  const uint32_t fS1 = upk + FP * KQ * 4;                                  // fixed column sums
+  const uint32_t fVf = fS1 + F * 4;                                        // fixed column V (f32)
+  const double pnc1 = a.p_fmean * (double)nc, pnc2 = a.p_emean * (double)nc;
+  uint64_t valid_cnt = 0, digest = 0;
+
+  // this wave's contiguous share of [rb, re)
+  const uint64_t nwaves = (uint64_t)gridDim.x * WPB;
+  const uint64_t gw = (uint64_t)blockIdx.x * WPB + wid;
+  const uint64_t total = a.re - a.rb;
+  uint64_t r = uni64(a.rb + (uint64_t)(((unsigned __int128)total * gw) / nwaves));
+  const uint64_t rend = uni64(a.rb + (uint64_t)(((unsigned __int128)total * (gw + 1)) / nwaves));
+
+  if (r < rend) {
+    uint32_t hq[F];  // fixed positions p_3 .. p_{N-1} (uniform)
+    uint64_t base = 0;
+    {
+      uint32_t p[N];
+      colex_unrank<N>(binom, a.ns, r, p);
+#pragma unroll
+      for (int k = 0; k < F; ++k) {
+        hq[k] = uni(p[3 + k]);
+        base += binom[hq[k] * (N + 1) + (k + 4)];
+      }
+      base = uni64(base);
+    }
+    uint64_t low = r - base;
+    for (;;) {
+      const uint64_t gend = base + uni64(binom[hq[0] * (N + 1) + 3]);
+      // ---------------- per-group, wave-uniform precompute -> group line
+      uint32_t freg[F];
+#pragma unroll
+      for (int k = 0; k < F; ++k) freg[k] = uni(a.srv_identity ? hq[k] : srv[hq[k]]);
+      if (lane < (uint32_t)F) {
+        uint32_t pos = 0;
+#pragma unroll
+        for (int k = 0; k < F; ++k) pos = lane == (uint32_t)k ? hq[k] : pos;
+        s32(fS1 + 4 * lane, cs1[pos]);
+        *(AS3 float*)(uintptr_t)(fVf + 4 * lane) = (float)vcol[pos];
+      }
+      if (lane < (uint32_t)FP) {
+        // rows 2*lane and 2*lane+1: sorted distances to the other fixed
+        // members (the self entry is INF, so it sorts last)
+        uint32_t v[2][PF];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const uint32_t k = 2 * lane + h;
+          uint32_t rk = 0;
+#pragma unroll
+          for (int kk = 0; kk < F; ++kk) rk = k == (uint32_t)kk ? freg[kk] : rk;
+#pragma unroll
+          for (int m = 0; m < PF; ++m) {
+            uint32_t d = 0xFFFFu;
+            if (m < F && k < (uint32_t)F && (uint32_t)m != k) d = l16(rqt + freg[m < F ? m : 0] * rstride + 2 * rk) >> LAT_SHIFT;
+            v[h][m] = d;
+          }
+          sort_network<PF>(v[h]);
+        }
+#pragma unroll
+        for (int i = 0; i < KQ; ++i) {
+          const uint32_t lo = i < F - 1 ? v[0][i < PF ? i : 0] : 0xFFFFu;
+          const uint32_t hi = i < F - 1 ? v[1][i < PF ? i : 0] : 0xFFFFu;
+          s32(upk + (lane * KQ + i) * 4, lo | (hi << 16));
+        }
+      }
+      // each client's nearest fixed member: latency << 4 | member index (3 + k)
+      for (uint32_t c = lane; c < (nq + 1) * 4; c += 64) {
+        uint32_t key = 3u;
+        if (c < nc) {
+          key = 0xFFFFu;
+#pragma unroll
+          for (int k = 0; k < F; ++k) key = min(key, l16(cqt + freg[k] * cstride + 2 * c) | (uint32_t)(3 + k));
+        }
+        s16(mfl + 2 * c, key);
+      }
+      wave_sync();
+
+      // ---------------- the group's configs, 64 per step
+      const uint64_t cend = uni64(gend < rend ? gend : rend);
+      uint32_t lp3 = a.lowtab[low + min((uint64_t)lane, cend - r - 1)];  // prefetched
+      while (r < cend) {
+        const uint32_t len = (uint32_t)min((uint64_t)64, cend - r);
+        bool have = lane < len;
+        const uint32_t cur = lp3;
+        {  // prefetch the next step's low part (the load overlaps this step)
+          const uint64_t nr = r + len;
+          if (nr < cend) lp3 = a.lowtab[low + len + min((uint64_t)lane, cend - nr - 1)];
+        }
+        uint64_t key[MAXOBJ];
+        bool ok[MAXOBJ];
+#pragma unroll
+        for (int o = 0; o < MAXOBJ; ++o) {
+          key[o] = 0;
+          ok[o] = false;
+        }
+        const uint64_t rank = r + lane;
+        if (have) {
+          uint32_t pv[3], rv[3];
+          pv[0] = cur & 0xFF;
+          pv[1] = (cur >> 8) & 0xFF;
+          pv[2] = cur >> 16;
+#pragma unroll
+          for (int i = 0; i < 3; ++i) rv[i] = a.srv_identity ? pv[i] : srv[pv[i]];
+          uint32_t cv[3];  // RQT column of each variable member
+#pragma unroll
+          for (int i = 0; i < 3; ++i) cv[i] = rqt + rv[i] * rstride;
+          // member m: 0..2 variable, 3.. fixed (config order = ascending positions)
+          uint32_t Q2[N], Q3[N];
+          uint32_t cS1p = 0, cS1e = 0;  // colocated sums: packed (t0 | t1 << 16), third table
+          uint32_t cS2[NL];
+#pragma unroll
+          for (int t = 0; t < NL; ++t) cS2[t] = 0;
+          // sorted row (packed pair: lo = member j, hi = member j + 1)
+          auto emit_pk = [&](int j, bool has_hi, const uint32_t* L) {
+            const uint32_t w0 = L[QC::lq(0) - 2], w1 = L[(NL >= 2 ? QC::lq(1) : QC::lq(0)) - 2];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+              if (h == 1 && !has_hi) break;
+              const uint32_t sel = h ? 0x07060302u : 0x05040100u;
+              const uint32_t sh = h ? 16u : 0u;
+              Q2[j + h] = (L[0] >> sh) & 0xFFFFu;
+              Q3[j + h] = (L[1] >> sh) & 0xFFFFu;
+              const uint32_t word = NL >= 2 ? __builtin_amdgcn_perm(w1, w0, sel) : ((w0 >> sh) & 0xFFFFu);
+              s32(qlane + ((uint32_t)(j + h) << GQSH), word);
+              cS1p += word;
+              const uint32_t q0 = word & 0xFFFFu;
+              cS2[0] += q0 * q0;
+              if (NL >= 2) {
+                const uint32_t q1 = word >> 16;
+                cS2[NL >= 2 ? 1 : 0] += q1 * q1;
+              }
+              if (NL == 3) {
+                const uint32_t q2 = (L[QC::lq(NL - 1) - 2] >> sh) & 0xFFFFu;
+                s32(qlane + ((uint32_t)(N + j + h) << GQSH), q2);
+                cS1e += q2;
+                cS2[NL - 1] += q2 * q2;
+              }
+            }
+          };
+          // ---- Q phase, variable rows 0 and 1 (packed), row 2 (lo half)
+          {
+            uint32_t v[PV];
+            // (stored latencies are << 4, so one shift of the packed pair is exact)
+            v[0] = (l16(cv[1] + 2 * rv[0]) | (l16(cv[0] + 2 * rv[1]) << 16)) >> LAT_SHIFT;  // d(0,1) | d(1,0)
+            v[1] = (l16(cv[2] + 2 * rv[0]) | (l16(cv[2] + 2 * rv[1]) << 16)) >> LAT_SHIFT;  // d(0,2) | d(1,2)
+#pragma unroll
+            for (int k = 0; k < F; ++k) {
+              const uint32_t fc = rqt + freg[k] * rstride;
+              v[2 + k] = (l16(fc + 2 * rv[0]) | (l16(fc + 2 * rv[1]) << 16)) >> LAT_SHIFT;
+            }
+#pragma unroll
+            for (int k = N - 1; k < PV; ++k) v[k] = 0xFFFFFFFFu;
+            sort_network_pk<PV>(v);
+            emit_pk(0, true, v);
+          }
+          {
+            uint32_t v[PV];
+            v[0] = l16(cv[0] + 2 * rv[2]) >> LAT_SHIFT;
+            v[1] = l16(cv[1] + 2 * rv[2]) >> LAT_SHIFT;
+#pragma unroll
+            for (int k = 0; k < F; ++k) v[2 + k] = l16(rqt + freg[k] * rstride + 2 * rv[2]) >> LAT_SHIFT;
+#pragma unroll
+            for (int k = N - 1; k < PV; ++k) v[k] = 0xFFFFu;
+            sort_network<PV>(v);
+            emit_pk(2, false, v);
+          }
+          // ---- fixed rows (pairs): insert the 3 lane distances into the
+          //      group's packed sorted lists
+#pragma unroll
+          for (int pp = 0; pp < FP; ++pp) {
+            uint32_t L[KQ];
+#pragma unroll
+            for (int i = 0; i < KQ; ++i) L[i] = l32(upk + (pp * KQ + i) * 4);
+            const bool has_hi = 2 * pp + 1 < F;
+#pragma unroll
+            for (int m = 0; m < 3; ++m) {
+              const uint32_t lo = l16(cv[m] + 2 * freg[2 * pp]);
+              const uint32_t hi = has_hi ? l16(cv[m] + 2 * freg[has_hi ? 2 * pp + 1 : 2 * pp]) : 0xFFF0u;
+              us2 x = as_us2((lo | (hi << 16)) >> LAT_SHIFT);
+              if (!has_hi) x = as_us2(as_u32(x) | 0xFFFF0000u);
+#pragma unroll
+              for (int i = 0; i < KQ; ++i) {
+                const us2 li = as_us2(L[i]);
+                L[i] = as_u32(pk_min(li, x));
+                if (i + 1 < KQ) x = pk_max(li, x);
+              }
+            }
+            emit_pk(3 + 2 * pp, has_hi, L);
+          }
+          // ---- FPaxos leader (f = 1, q = 2, min COV, first in config order)
+          auto pos_of = [&](int l) { return l < 3 ? pv[l] : hq[l - 3]; };
+          auto reg_of = [&](int l) { return l < 3 ? rv[l] : freg[l - 3]; };
+          auto s1_of = [&](int l) { return l < 3 ? cs1[pv[l]] : l32(fS1 + 4 * (l - 3)); };
+          auto vf_of = [&](int l) { return l < 3 ? (float)vcol[pv[l]] : lf32(fVf + 4 * (l - 3)); };
+          uint32_t bi = 0, bpos = pv[0];
+          bool amb = false;
+          uint32_t bS = s1_of(0) + nc * Q2[0];
+          float bV = vf_of(0);
+#pragma unroll
+          for (int l = 1; l < N; ++l) {
+            const uint32_t S = s1_of(l) + nc * Q2[l];
+            const float V = vf_of(l);
+            if (V == 0.0f && bV == 0.0f) continue;  // both COV exactly 0: keep the first
+            const uint32_t pl = pos_of(l);
+            const int c = cov2_sign(V, S, bV, bS, [&] { return vcol[pl]; }, [&] { return vcol[bpos]; });
+            if (c == 0) amb = true;
+            if (c < 0) {
+              bi = l;
+              bS = S;
+              bV = V;
+              bpos = pl;
+            }
+          }
+          if (amb) {
+            defer_rank(a, rank);
+            have = false;
+          }
+          if (have) {
+            uint32_t lpos = pv[0], lq2 = Q2[0], lq3 = Q3[0], lreg = rv[0];
+#pragma unroll
+            for (int l = 1; l < N; ++l)
+              if (bi == (uint32_t)l) {
+                lpos = pos_of(l);
+                lq2 = Q2[l];
+                lq3 = Q3[l];
+                lreg = reg_of(l);
+              }
+            Mom mom[NSLOT];
+            // ---- Input leaderless: 3 lane columns + the wave's nearest-fixed line
+            {
+              const us2 ones = {1, 1};
+              const us2 J1 = {1, 1}, J2 = {2, 2};
+              uint32_t S1[NL], s2[NL];
+              uint64_t S2[NL];
+#pragma unroll
+              for (int t = 0; t < NL; ++t) {
+                S1[t] = 0;
+                S2[t] = 0;
+                s2[t] = 0;
+              }
+              const uint32_t c0 = cqt + rv[0] * cstride, c1 = cqt + rv[1] * cstride, c2 = cqt + rv[2] * cstride;
+              auto quad = [&](uint32_t g8, uint32_t mlo, uint32_t mhi) {
+                const uint2 wa = l64(c0 + g8), wb = l64(c1 + g8), wc = l64(c2 + g8), wf = l64(mfl + g8);
+                const us2 lo = pk_min(pk_min(as_us2(wa.x), as_us2(wb.x) | J1), pk_min(as_us2(wc.x) | J2, as_us2(wf.x)));
+                const us2 hi = pk_min(pk_min(as_us2(wa.y), as_us2(wb.y) | J1), pk_min(as_us2(wc.y) | J2, as_us2(wf.y)));
+                const uint32_t L = as_u32(lo), H = as_u32(hi);
+                constexpr int NQ = NL == 3 ? 8 : 4;
+                uint32_t q[NQ];
+                q[0] = l32(qlane + ((L & 15u) << GQSH));
+                q[1] = l32(qlane + (((L >> 16) & 15u) << GQSH));
+                q[2] = l32(qlane + ((H & 15u) << GQSH));
+                q[3] = l32(qlane + (((H >> 16) & 15u) << GQSH));
+                if (NL == 3) {
+                  const uint32_t P2 = qlane + ((uint32_t)N << GQSH);
+                  q[NQ - 4] = l32(P2 + ((L & 15u) << GQSH));
+                  q[NQ - 3] = l32(P2 + (((L >> 16) & 15u) << GQSH));
+                  q[NQ - 2] = l32(P2 + ((H & 15u) << GQSH));
+                  q[NQ - 1] = l32(P2 + (((H >> 16) & 15u) << GQSH));
+                }
+                const us2 dlo = lo >> (us2)4, dhi = hi >> (us2)4;
+                auto acc1 = [&](int t, uint32_t ql01, uint32_t ql23) {
+                  us2 a01 = dlo + as_us2(ql01), a23 = dhi + as_us2(ql23);
+                  a01 = as_us2(as_u32(a01) & mlo);
+                  a23 = as_us2(as_u32(a23) & mhi);
+                  S1[t] = __builtin_amdgcn_udot2(a01, ones, S1[t], false);
+                  S1[t] = __builtin_amdgcn_udot2(a23, ones, S1[t], false);
+                  s2[t] = __builtin_amdgcn_udot2(a01, a01, s2[t], false);
+                  s2[t] = __builtin_amdgcn_udot2(a23, a23, s2[t], false);
+                };
+                acc1(0, __builtin_amdgcn_perm(q[1], q[0], 0x05040100u), __builtin_amdgcn_perm(q[3], q[2], 0x05040100u));
+                if (NL >= 2)
+                  acc1(NL >= 2 ? 1 : 0, __builtin_amdgcn_perm(q[1], q[0], 0x07060302u),
+                       __builtin_amdgcn_perm(q[3], q[2], 0x07060302u));
+                if (NL == 3)
+                  acc1(NL - 1, __builtin_amdgcn_perm(q[NQ - 3], q[NQ - 4], 0x05040100u),
+                       __builtin_amdgcn_perm(q[NQ - 1], q[NQ - 2], 0x05040100u));
+              };
+              auto flush = [&]() {
+#pragma unroll
+                for (int t = 0; t < NL; ++t) {
+                  S2[t] += s2[t];
+                  s2[t] = 0;
+                }
+              };
+              const uint32_t nql = (a.ablate & 1) ? 0u : nq;
+              for (uint32_t g0 = 0; g0 < nql; g0 += a.s2_flush) {
+                const uint32_t ge = min(nql, g0 + a.s2_flush);
+#pragma unroll 4
+                for (uint32_t g = g0; g < ge; ++g) quad(g * 8, ~0u, ~0u);
+                flush();
+              }
+              if (rem && !(a.ablate & 1)) {
+                quad(nq * 8, rem >= 2 ? ~0u : 0x0000FFFFu, rem == 3 ? 0x0000FFFFu : 0u);
+                flush();
+              }
+              if (a.ablate & 1) {  // timing only: non-degenerate dummy sums
+#pragma unroll
+                for (int t = 0; t < NL; ++t) {
+                  S1[t] = 1000u + rv[0] + t;
+                  S2[t] = (uint64_t)S1[t] * S1[t] + 12345u;
+                }
+              }
+              mom[SLOT_AF1] = Mom{S1[QC::idx_a1], S2[QC::idx_a1], nc};
+              mom[SLOT_AF2] = Mom{S1[QC::idx_a2], S2[QC::idx_a2], nc};
+              mom[SLOT_E] = Mom{S1[QC::idx_e], S2[QC::idx_e], nc};
+            }
+            // ---- Input FPaxos from the leader column's sums
+            const uint32_t lc1 = cs1[lpos];
+            const uint64_t lc2 = cs2[lpos];
+            mom[SLOT_FF1] = leader_mom(lc1, lc2, nc, lq2);
+            mom[SLOT_FF2] = leader_mom(lc1, lc2, nc, lq3);
+            // ---- Colocated: FPaxos reads the leader's column of the config
+            //      submatrix; leaderless values are the members' own quorums
+            {
+              const uint32_t lcol = rqt + lreg * rstride;
+              uint32_t f1 = 0, f1s = 0, f2 = 0, f2s = 0;
+#pragma unroll
+              for (int k = 0; k < N; ++k) {
+                const uint32_t v = l16(lcol + 2 * reg_of(k)) >> LAT_SHIFT;
+                const uint32_t x1 = v + lq2, x2 = v + lq3;
+                f1 += x1;
+                f1s += x1 * x1;
+                f2 += x2;
+                f2s += x2 * x2;
+              }
+              mom[5 + SLOT_FF1] = Mom{f1, f1s, (uint32_t)N};
+              mom[5 + SLOT_FF2] = Mom{f2, f2s, (uint32_t)N};
+              const uint32_t cl1[3] = {cS1p & 0xFFFFu, cS1p >> 16, cS1e};
+              mom[5 + SLOT_AF1] = Mom{cl1[QC::idx_a1], cS2[QC::idx_a1], (uint32_t)N};
+              mom[5 + SLOT_AF2] = Mom{cl1[QC::idx_a2], cS2[QC::idx_a2], (uint32_t)N};
+              mom[5 + SLOT_E] = Mom{cl1[QC::idx_e], cS2[QC::idx_e], (uint32_t)N};
+            }
+            const double vlead = vcol[lpos];
+            if (DEF) {
+              // ---- compute_score validity (search.rs:421-472), exact
+              bool valid = false;
+              const int fcap = min(N / 2, a.ft_metric);
+              bool defer = false;
+              if (a.want_score) {
+                valid = true;
+#pragma unroll
+                for (int f = 1; f <= 2; ++f) {
+                  if (f > fcap) break;
+                  const Mom& ma = mom[f == 1 ? SLOT_AF1 : SLOT_AF2];
+                  const Mom& mf = mom[f == 1 ? SLOT_FF1 : SLOT_FF2];
+                  // fmi >= p1: integers unless the sums meet exactly
+                  const int64_t D = (int64_t)mf.s1 - (int64_t)ma.s1;
+                  bool mok;
+                  if (a.p_int && (double)D != pnc1) mok = (double)D > pnc1;
+                  else mok = (mom_mean(mf) - mom_mean(ma)) >= a.p_fmean;
+                  valid = valid && mok;
+                  if (valid) {
+                    // cov_f >= cov_a (min_fairness_fpaxos_improv == 0 on this path)
+                    const uint64_t Va = mom_v(ma);
+                    if (!(vlead == 0.0 && Va == 0)) {
+                      const int c = cov2_sign((float)vlead, (uint32_t)mf.s1, (float)Va, (uint32_t)ma.s1,
+                                              [&] { return vlead; }, [&] { return (double)Va; });
+                      if (c == 0) defer = true;
+                      valid = valid && c > 0;
+                    }
+                  }
+                  if (N == 11 || N == 13) {
+                    const int64_t De = (int64_t)mom[SLOT_E].s1 - (int64_t)ma.s1;
+                    bool eok;
+                    if (a.p_int && (double)De != pnc2) eok = (double)De > pnc2;
+                    else eok = (mom_mean(mom[SLOT_E]) - mom_mean(ma)) >= a.p_emean;
+                    valid = valid && eok;
+                  }
+                }
+              }
+              if (defer) {
+                defer_rank(a, rank);
+              } else {
+                if (valid) ++valid_cnt;
+                if (a.want_digest && !(a.ablate & 16)) {
+                  uint32_t h = 0;
+#pragma unroll
+                  for (int sl = 0; sl < NSLOT; ++sl) h = digest_fold(h, mom[sl].s1, mom[sl].s2);
+                  digest += digest_final(rank, bi, h);
+                }
+                // ---- default objectives: 0 SCORE, 1 MEAN af1, 2 MEAN ff1, 3 COV af1, 4 MEAN e
+                ok[1] = ok[2] = ok[4] = true;
+                key[1] = mom[SLOT_AF1].s1;
+                key[2] = mom[SLOT_FF1].s1;
+                key[4] = mom[SLOT_E].s1;
+                if (valid) {
+                  const uint64_t tkey = tk.thr[0].key;
+                  bool maybe = tkey == ~0ull;
+                  if (!maybe) {
+                    const uint64_t ob = ~tkey;
+                    const uint64_t bits = (ob >> 63) ? (ob & 0x7FFFFFFFFFFFFFFFull) : ~ob;
+                    const double tscore = __longlong_as_double((long long)bits);
+                    int64_t T = 0;
+#pragma unroll
+                    for (int f = 1; f <= 2; ++f) {
+                      if (f > fcap) break;
+                      const int64_t a1 = (int64_t)mom[f == 1 ? SLOT_AF1 : SLOT_AF2].s1;
+                      T += (int64_t)mom[f == 1 ? SLOT_FF1 : SLOT_FF2].s1 - a1 + 30 * ((int64_t)mom[SLOT_E].s1 - a1);
+                    }
+                    maybe = !(tscore == tscore) || (double)T >= (tscore - 1e-6) * (double)nc;
+                  }
+                  if (maybe) {
+                    double score = 0.0;
+                    const double me = mom_mean(mom[SLOT_E]);
+#pragma unroll
+                    for (int f = 1; f <= 2; ++f) {
+                      if (f > fcap) break;
+                      const double mA = mom_mean(mom[f == 1 ? SLOT_AF1 : SLOT_AF2]);
+                      const double fmi = mom_mean(mom[f == 1 ? SLOT_FF1 : SLOT_FF2]) - mA;
+                      const double emi = me - mA;
+                      double t = 30.0 * emi;
+                      t = fmi + t;
+                      score = score + t;
+                    }
+                    ok[0] = true;
+                    key[0] = ~orderable_f64(score);
+                  }
+                }
+                {
+                  const Mom& m = mom[SLOT_AF1];
+                  const uint64_t tk3 = tk.thr[3].key;
+                  const uint64_t V = mom_v(m);
+                  // f32 screen with a 2^-10 margin (conservative: offers a superset)
+                  const float S = (float)m.s1;
+                  const bool maybe = tk3 == ~0ull ||
+                                     (float)V <= (float)__longlong_as_double((long long)tk3) * (S * S) * (1.0f + 0x1p-10f);
+                  if (maybe) {
+                    ok[3] = true;
+                    key[3] = cov_key(m);
+                  }
+                }
+              }
+            } else {
+              if (!finish_config<N>(a, mom, vlead, bi, rank, tk.thr, pnc1, pnc2, valid_cnt, digest, key, ok))
+                defer_rank(a, rank);
+            }
+          }
+        }
+        // ---- top-K: lock-free screen, exact merge under the block lock
+        if (!(a.ablate & 4)) {
+          const int nobj = DEF ? 5 : a.n_obj;
+          bool pass = false;
+#pragma unroll
+          for (int o = 0; o < MAXOBJ; ++o)
+            if (o < nobj) pass = pass || (ok[o] && key[o] <= tk.thr[o].key);
+          if (__ballot(pass)) wave_topk(tk, lock, nobj, a.K, key, ok, rank);
+        }
+        r += len;
+        low += len;
+      }
+      if (r >= rend) break;
+      // ---------------- next group: colex successor of the fixed positions
+      // (a combination of {3 .. ns-1}; the smallest fixed position is >= 3)
+      {
+        int js = F;
+#pragma unroll
+        for (int k = F - 1; k >= 0; --k) {
+          const uint32_t nxt = (k == F - 1) ? a.ns : hq[k + 1];
+          if (hq[k] + 1 < nxt) js = k;
+        }
+        base = 0;
+#pragma unroll
+        for (int k = 0; k < F; ++k) {
+          hq[k] = uni(k < js ? (uint32_t)(3 + k) : (k == js ? hq[k] + 1 : hq[k]));
+          base += binom[hq[k] * (N + 1) + (k + 4)];
+        }
+        base = uni64(base);
+        low = 0;
+      }
+      wave_sync();  // the group line is rewritten next
+    }
+  }
+  if (valid_cnt) atomicAdd(&a.out_counters[0], (unsigned long long)valid_cnt);
+  if (digest) atomicAdd(&a.out_counters[1], (unsigned long long)digest);
+  __syncthreads();
+  Rec* dst = a.out_top + (size_t)blockIdx.x * a.n_obj * KP;
+  for (uint32_t i = tid; i < (uint32_t)a.n_obj * KP; i += FAST_BD) dst[i] = tk.top[i];
+}
+
+// ------------------------------------------------------------- launcher ---
+template <int N, bool DEF>
+static hipError_t launch_group_n(const FastArgs& a, uint32_t grid, size_t shm, hipStream_t st) {
+  auto k = sweep_group_kernel<N, DEF>;
+  hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k, dim3(grid), dim3(FAST_BD), shm, st, a);
+  return hipGetLastError();
+}
+
+static const void* group_fn(uint32_t n, bool def) {
+  switch (n) {
+#define FN_CASE(NN) \
+  case NN: return def ? (const void*)sweep_group_kernel<NN, true> : (const void*)sweep_group_kernel<NN, false>;
+    FN_CASE(4) FN_CASE(5) FN_CASE(6) FN_CASE(7) FN_CASE(8) FN_CASE(9) FN_CASE(10) FN_CASE(11) FN_CASE(12)
+    FN_CASE(13) FN_CASE(14) FN_CASE(15) FN_CASE(16)
+#undef FN_CASE
+    default: return nullptr;
+  }
+}
+
+int group_occupancy(uint32_t n, size_t shm, bool def) {
+  int nb = 0;
+  const void* k = group_fn(n, def);
+  if (!k) return 0;
+  if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm) != hipSuccess) return 1;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, (int)FAST_BD, shm) != hipSuccess) return 1;
+  return nb > 0 ? nb : 1;
+}
+
+hipError_t launch_group(const FastArgs& a, uint32_t n, bool def, uint32_t grid, size_t shm, hipStream_t st) {
+  switch (n) {
+#define GS_CASE(NN) \
+  case NN: return def ? launch_group_n<NN, true>(a, grid, shm, st) : launch_group_n<NN, false>(a, grid, shm, st);
+    GS_CASE(4) GS_CASE(5) GS_CASE(6) GS_CASE(7) GS_CASE(8) GS_CASE(9) GS_CASE(10) GS_CASE(11) GS_CASE(12)
+    GS_CASE(13) GS_CASE(14) GS_CASE(15) GS_CASE(16)
+#undef GS_CASE
+    default: return hipErrorInvalidValue;
+  }
+}
+
+}  // namespace bote

@@ -94,6 +94,9 @@ struct FastArgs {
   Rec* out_top;
   unsigned long long* out_counters;
   int want_digest;
+  // group kernel (bote_group.hip): packed (p0 | p1 << 8 | p2 << 16) of the
+  // 3-subsets of positions in colex order (the low part of a group's ranks)
+  const uint32_t* lowtab;
   uint64_t* queue;  // deferred near-tie configs (colex ranks)
   unsigned long long* queue_count;
   uint64_t queue_cap;
@@ -104,6 +107,9 @@ struct FastArgs {
 size_t fast_smem_bytes(const FastArgs& a, uint32_t n);
 int fast_occupancy(uint32_t n, size_t shm);
 hipError_t launch_fast(const FastArgs& a, uint32_t n, uint32_t grid, size_t shm, hipStream_t st);
+size_t group_smem_bytes(const FastArgs& a, uint32_t n);
+int group_occupancy(uint32_t n, size_t shm, bool def_objectives);
+hipError_t launch_group(const FastArgs& a, uint32_t n, bool def_objectives, uint32_t grid, size_t shm, hipStream_t st);
 
 size_t eval_smem_bytes(const EvalArgs& a, uint32_t n, uint32_t bd, bool topk);
 int eval_occupancy(uint32_t n, bool full, uint32_t bd, size_t shm);

@@ -23,7 +23,7 @@
 // V = nc*sum(L^2) - (sum L)^2 of its column, precomputed per position); the
 // Input leaderless keys by the packed client-quad loop; compute_score validity
 // by integer / f64-margin decisions; digest; block top-K.
-#include "bote_kernels.hpp"
+#include "bote_fast.hpp"
 
 #ifndef BOTE_QROW_BARRIER
 #define BOTE_QROW_BARRIER 1
@@ -31,9 +31,6 @@
 
 namespace bote {
 
-typedef unsigned short us2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ us2 as_us2(uint32_t x) { return __builtin_bit_cast(us2, x); }
-__device__ __forceinline__ uint32_t as_u32(us2 x) { return __builtin_bit_cast(uint32_t, x); }
 
 constexpr uint32_t QSH = 10;  // log2(FAST_BD * 4): byte stride between qtab member planes
 static_assert((1u << QSH) == FAST_BD * 4, "qtab plane stride");
@@ -90,9 +87,6 @@ __device__ __forceinline__ uint32_t sel_u(const uint32_t (&arr)[N], uint32_t i) 
   return r;
 }
 
-__device__ __forceinline__ uint32_t ld16(const unsigned char* b, uint32_t off) { return *(const uint16_t*)(b + off); }
-__device__ __forceinline__ uint32_t ld32(const unsigned char* b, uint32_t off) { return *(const uint32_t*)(b + off); }
-__device__ __forceinline__ uint2 ld64(const unsigned char* b, uint32_t off) { return *(const uint2*)(b + off); }
 
 // ------------------------------------------------------------ hot loop ----
 // Input leaderless keys over client quads.  Per quad and member: one
@@ -404,10 +398,8 @@ __global__ void __launch_bounds__(FAST_BD, 4) sweep_fast_kernel(FastArgs a) {
             }
           }
         }
-        if (amb) {
-          // defer to the exact generic kernel (see bote_sweep_launch)
-          unsigned long long q = atomicAdd(a.queue_count, 1ull);
-          if (q < a.queue_cap) a.queue[q] = rank;
+        if (amb) {  // defer to the exact generic kernel (see bote_sweep_launch)
+          defer_rank(a, rank);
           have = false;
         }
         if (have) {
@@ -430,13 +422,8 @@ __global__ void __launch_bounds__(FAST_BD, 4) sweep_fast_kernel(FastArgs a) {
             mom[SLOT_E] = Mom{S1[QC::idx_e], S2[QC::idx_e], nc};
           }
           // Input FPaxos: moments from the leader column's sums
-          {
-            const uint64_t c1 = s.cs1[lp], c2 = s.cs2[lp];
-            uint64_t q = lq2;
-            mom[SLOT_FF1] = Mom{c1 + (uint64_t)nc * q, c2 + 2ull * q * c1 + (uint64_t)nc * q * q, nc};
-            q = lq3;
-            mom[SLOT_FF2] = Mom{c1 + (uint64_t)nc * q, c2 + 2ull * q * c1 + (uint64_t)nc * q * q, nc};
-          }
+          mom[SLOT_FF1] = leader_mom(s.cs1[lp], s.cs2[lp], nc, lq2);
+          mom[SLOT_FF2] = leader_mom(s.cs1[lp], s.cs2[lp], nc, lq3);
           // Colocated: leaderless values are the members' own quorum latencies;
           // FPaxos reads the leader's column of the config submatrix.
           {
@@ -456,119 +443,9 @@ __global__ void __launch_bounds__(FAST_BD, 4) sweep_fast_kernel(FastArgs a) {
             mom[5 + SLOT_AF2] = Mom{cS1[QC::idx_a2], cS2[QC::idx_a2], (uint32_t)N};
             mom[5 + SLOT_E] = Mom{cS1[QC::idx_e], cS2[QC::idx_e], (uint32_t)N};
           }
-          // ---- compute_score validity and score (search.rs:421-472)
-          bool valid = false;
-          const int fcap = min(N / 2, a.ft_metric);
-          if (a.want_score && !(a.ablate & 8)) {
-            valid = true;
-#pragma unroll
-            for (int f = 1; f <= 2; ++f) {
-              if (f > fcap) break;
-              const Mom& ma = mom[f == 1 ? SLOT_AF1 : SLOT_AF2];
-              const Mom& mf = mom[f == 1 ? SLOT_FF1 : SLOT_FF2];
-              // fmi >= p1: exact in integers unless the sums meet exactly
-              const double D = (double)(int64_t)(mf.s1 - ma.s1);
-              bool mok;
-              if (a.p_int && D != pnc1) mok = D > pnc1;
-              else mok = (mom_mean(mf) - mom_mean(ma)) >= a.p_fmean;
-              valid = valid && mok;
-              if (valid) {
-                // cov_f >= cov_a  <=>  V_f * S1_a^2 >= V_a * S1_f^2
-                const double Vf = s.vcol[lp];
-                const double Va = (double)mom_v(ma);
-                const double sa = (double)ma.s1 * (double)ma.s1, sf = (double)mf.s1 * (double)mf.s1;
-                const double x = Vf * sa, y = Va * sf;
-                if (!(Vf == 0.0 && Va == 0.0)) {
-                  const double d = x - y, tol = 0x1p-32 * fmax(x, y);
-                  if (fabs(d) <= tol) amb = true;
-                  valid = valid && d > 0.0;
-                }
-              }
-              if (N == 11 || N == 13) {
-                const double De = (double)(int64_t)(mom[SLOT_E].s1 - ma.s1);
-                bool eok;
-                if (a.p_int && De != pnc2) eok = De > pnc2;
-                else eok = (mom_mean(mom[SLOT_E]) - mom_mean(ma)) >= a.p_emean;
-                valid = valid && eok;
-              }
-            }
-          }
-          if (amb) {
-            unsigned long long q = atomicAdd(a.queue_count, 1ull);
-            if (q < a.queue_cap) a.queue[q] = rank;
+          if (!finish_config<N>(a, mom, s.vcol[lp], bi, rank, s.tk.thr, pnc1, pnc2, valid_cnt, digest, key, ok)) {
+            defer_rank(a, rank);
             have = false;
-          } else {
-            if (valid) ++valid_cnt;
-            if (a.want_digest && !(a.ablate & 16)) {
-              uint32_t h = 0;
-#pragma unroll
-              for (int sl = 0; sl < NSLOT; ++sl)
-                if (QC::maxf >= 2 || (sl % 5 != SLOT_AF2 && sl % 5 != SLOT_FF2))
-                  h = digest_fold(h, mom[sl].s1, mom[sl].s2);
-              digest += digest_final(rank, bi, h);
-            }
-            // ---- objective keys
-#pragma unroll
-            for (int o = 0; o < MAXOBJ; ++o) {
-              if (o >= a.n_obj) break;
-              const uint32_t kind = a.obj_kind[o], sl = a.obj_slot[o];
-              if (kind == OBJ_SCORE) {
-                if (!valid) continue;
-                // score * nc = sum_f (S1_ff - S1_af) + 30 (S1_e - S1_af) exactly;
-                // the f64 score (search.rs:445-468) is within 1e-9 of it, so it
-                // is computed only when it may beat the objective's threshold.
-                const Rec th = s.tk.thr[o];
-                bool maybe = th.key == ~0ull;
-                if (!maybe) {
-                  const uint64_t ob = ~th.key;  // orderable bits of the threshold score
-                  const uint64_t bits = (ob >> 63) ? (ob & 0x7FFFFFFFFFFFFFFFull) : ~ob;
-                  const double tscore = __longlong_as_double((long long)bits);
-                  int64_t T = 0;
-#pragma unroll
-                  for (int f = 1; f <= 2; ++f) {
-                    if (f > fcap) break;
-                    const int64_t a1 = (int64_t)mom[f == 1 ? SLOT_AF1 : SLOT_AF2].s1;
-                    T += (int64_t)mom[f == 1 ? SLOT_FF1 : SLOT_FF2].s1 - a1 + 30 * ((int64_t)mom[SLOT_E].s1 - a1);
-                  }
-                  maybe = !(tscore == tscore) || (double)T >= (tscore - 1e-6) * (double)nc;
-                }
-                if (maybe) {
-                  double score = 0.0;
-                  const double me = mom_mean(mom[SLOT_E]);
-#pragma unroll
-                  for (int f = 1; f <= 2; ++f) {
-                    if (f > fcap) break;
-                    const double mA = mom_mean(mom[f == 1 ? SLOT_AF1 : SLOT_AF2]);
-                    const double fmi = mom_mean(mom[f == 1 ? SLOT_FF1 : SLOT_FF2]) - mA;
-                    const double emi = me - mA;
-                    double t = 30.0 * emi;
-                    t = fmi + t;
-                    score = score + t;
-                  }
-                  ok[o] = true;
-                  key[o] = ~orderable_f64(score);
-                }
-                continue;
-              }
-#pragma unroll
-              for (int q = 0; q < NSLOT; ++q) {
-                if ((uint32_t)q != sl) continue;
-                const Mom& m = mom[q];
-                if (kind == OBJ_MEAN) {
-                  ok[o] = true;
-                  key[o] = m.s1;
-                } else {
-                  // COV key fl(V / S1^2): divide only when it may beat the threshold
-                  const uint64_t tk = s.tk.thr[o].key;
-                  const double V = (double)mom_v(m), S = (double)m.s1 * (double)m.s1;
-                  const bool maybe = tk == ~0ull || V <= __longlong_as_double((long long)tk) * S * (1.0 + 0x1p-40);
-                  if (maybe) {
-                    ok[o] = true;
-                    key[o] = cov_key(m);
-                  }
-                }
-              }
-            }
           }
         }
       }

@@ -202,8 +202,9 @@ int bote_sweep_last_kernel_ms(bote_sweep* s, float* out_ms);
  * launch since the last bote_sweep_timing_reset; synchronises on the last. */
 int bote_sweep_timing_reset(bote_sweep* s);
 int bote_sweep_timing(bote_sweep* s, float* out_total_ms, uint32_t* out_launches);
-/* 1 when the sweep runs the packed fast-path kernel (bote_sweep.hip), 0 for
- * the generic kernel; both are exact (DESIGN.md "Kernels"). */
+/* Which sweep kernel runs: 0 the generic kernel (bote_kernels.hip), 1 the
+ * packed fast-path kernel (bote_sweep.hip), 2 the group kernel
+ * (bote_group.hip).  All are exact (DESIGN.md "Kernels"). */
 int bote_sweep_is_fast(const bote_sweep* s, int* out);
 /* Launch geometry chosen at creation (persistent grid, block size, LDS bytes). */
 int bote_sweep_grid(const bote_sweep* s, uint32_t* out_grid, uint32_t* out_block, uint32_t* out_lds_bytes);

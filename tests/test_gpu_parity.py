@@ -339,14 +339,17 @@ def test_r128_n6_subrange_and_max_latency():
 
 
 # ------------------------------------------------ fast path vs generic ----
-def _sweep(dp, srv, cli, n, rb, re, K=100, ranking=DEFAULT_RANKING, generic=False):
-    if generic:
-        os.environ["BOTE_FORCE_GENERIC"] = "1"
+def _sweep(dp, srv, cli, n, rb, re, K=100, ranking=DEFAULT_RANKING, generic=False, kernel=None):
+    """kernel: None (default choice), 'generic', 'fast' or 'group' (BOTE_SWEEP_KERNEL)."""
+    kernel = "generic" if generic else kernel
+    if kernel:
+        os.environ["BOTE_SWEEP_KERNEL"] = kernel
     try:
         sw = Sweep(dp, srv, cli, n, DEFAULT_OBJECTIVES, K=K, ranking=ranking, digest=True)
     finally:
-        os.environ.pop("BOTE_FORCE_GENERIC", None)
-    assert sw.is_fast() == (not generic)
+        os.environ.pop("BOTE_SWEEP_KERNEL", None)
+    if kernel:
+        assert sw.kernel_path() == (kernel if not (kernel == "group" and n < 4) else "fast")
     sw.launch(rb, re)
     return sw.result()
 
@@ -355,19 +358,44 @@ def test_fast_path_equals_generic_path():
     p = Planet.synthetic(64)
     dp = DevicePlanet(p)
     srv = np.arange(64, dtype=np.uint32)
-    for n, rb, re in ((7, 10_000_000, 12_000_000), (6, 0, 3_000_000), (4, 0, _lib.binomial(64, 4))):
-        a = _sweep(dp, srv, srv, n, rb, re)
+    for n, rb, re in ((7, 10_000_000, 12_000_000), (6, 0, 3_000_000), (4, 0, _lib.binomial(64, 4)),
+                      (9, 123_456_789, 124_456_789)):
         b = _sweep(dp, srv, srv, n, rb, re, generic=True)
-        assert (a.valid, a.digest, a.tops) == (b.valid, b.digest, b.tops)
+        for k in ("fast", "group"):
+            a = _sweep(dp, srv, srv, n, rb, re, kernel=k)
+            assert (a.valid, a.digest, a.tops) == (b.valid, b.digest, b.tops), k
     # a client subset (separate region-quad matrix) and a ragged client count
     g = Planet.new()
     gdp = DevicePlanet(g)
     gs = np.arange(g.R, dtype=np.uint32)
     for cli in (np.array([3, 1, 4, 15, 9, 2, 6], np.uint32), np.arange(0, 20, 2, dtype=np.uint32)):
         for n in (3, 5, 8):
-            a = _sweep(gdp, gs, cli, n, 0, _lib.binomial(g.R, n))
             b = _sweep(gdp, gs, cli, n, 0, _lib.binomial(g.R, n), generic=True)
-            assert (a.valid, a.digest, a.tops) == (b.valid, b.digest, b.tops)
+            for k in ("fast", "group"):
+                a = _sweep(gdp, gs, cli, n, 0, _lib.binomial(g.R, n), kernel=k)
+                assert (a.valid, a.digest, a.tops) == (b.valid, b.digest, b.tops), k
+
+
+def test_group_kernel_custom_objectives():
+    """Objective sets other than the default run the group kernel's generic
+    key path (finish_config); it must equal the generic kernel."""
+    p = Planet.synthetic(64)
+    dp = DevicePlanet(p)
+    srv = np.arange(64, dtype=np.uint32)
+    objs = [(_lib.OBJ_COV, _lib.SLOT_AF2), (_lib.OBJ_MEAN, 5 + _lib.SLOT_FF2), (_lib.OBJ_SCORE, 0),
+            (_lib.OBJ_COV, 5 + _lib.SLOT_E), (_lib.OBJ_MEAN, _lib.SLOT_AF1), (_lib.OBJ_COV, _lib.SLOT_FF1)]
+    out = {}
+    for k in ("generic", "group"):
+        os.environ["BOTE_SWEEP_KERNEL"] = k
+        try:
+            sw = Sweep(dp, srv, srv, 7, objs, K=50, ranking=DEFAULT_RANKING, digest=True)
+        finally:
+            os.environ.pop("BOTE_SWEEP_KERNEL", None)
+        assert sw.kernel_path() == k
+        sw.launch(200_000_000, 201_500_000)
+        r = sw.result()
+        out[k] = (r.valid, r.digest, r.tops)
+    assert out["group"] == out["generic"]
 
 
 def test_fast_path_deferral_equidistant():
@@ -380,10 +408,11 @@ def test_fast_path_deferral_equidistant():
     rp = RankingParams.new(0, 0, 0, 0, 3, 13, FTMetric.F1F2)
     for n in (3, 5):
         total = _lib.binomial(p.R, n)
-        got = _sweep(dp, srv, srv, n, 0, total, ranking=rp)
         tops, valid, digest = _oracle_sweep(o, srv, srv, n, 0, total, DEFAULT_OBJECTIVES, 100, rp)
-        assert (got.valid, got.digest) == (valid, digest)
-        assert got.tops == [list(t) for t in tops]
+        for k in ("fast", "group"):
+            got = _sweep(dp, srv, srv, n, 0, total, ranking=rp, kernel=k)
+            assert (got.valid, got.digest) == (valid, digest)
+            assert got.tops == [list(t) for t in tops]
 
 
 def test_fast_path_deferral_overflow():
@@ -395,7 +424,8 @@ def test_fast_path_deferral_overflow():
     srv = np.arange(p.R, dtype=np.uint32)
     total = _lib.binomial(p.R, 5)
     assert total > (1 << 20)
-    got = _sweep(dp, srv, srv, 5, 0, total)
     tops, valid, digest = _oracle_sweep(o, srv, srv, 5, 0, total, DEFAULT_OBJECTIVES, 100, DEFAULT_RANKING)
-    assert (got.valid, got.digest) == (valid, digest)
-    assert got.tops == [list(t) for t in tops]
+    for k in ("fast", "group"):
+        got = _sweep(dp, srv, srv, 5, 0, total, kernel=k)
+        assert (got.valid, got.digest) == (valid, digest)
+        assert got.tops == [list(t) for t in tops]
