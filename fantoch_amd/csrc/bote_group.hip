@@ -38,6 +38,11 @@
 namespace bote {
 
 constexpr int WPB = FAST_BD / 64;  // wavefronts per workgroup
+// waves per SIMD the register allocation targets (5: <= 96 VGPRs; LDS per
+// workgroup stays under 32 KB at R = 64, so 5 workgroups fit a CU)
+#ifndef BOTE_GROUP_WAVES
+#define BOTE_GROUP_WAVES 5
+#endif
 constexpr uint32_t GQSH = 10;      // log2(FAST_BD * 4): byte stride between qtab member planes
 static_assert((1u << GQSH) == FAST_BD * 4, "qtab plane stride");
 
@@ -69,7 +74,7 @@ __host__ __device__ inline size_t group_layout(const FastArgs& a, int N, int NLW
   o = (o + 15) & ~(size_t)15;
   off[5] = o; o += (size_t)a.ns * 8;                   // cs2
   off[6] = o; o += (size_t)a.ns * 8;                   // vcol (f64)
-  off[7] = o; o += (size_t)(a.ns + 1) * (N + 1) * 8;  // binom
+  off[7] = o;  // (binomials stay in global memory: uniform scalar loads, once per group)
   off[8] = o; o += (size_t)WPB * gline_bytes(a, N, KQ);  // per-wave group lines
   o = (o + 15) & ~(size_t)15;
   off[9] = o; o += (size_t)a.n_obj * KP * 16;  // top
@@ -217,7 +222,7 @@ __device__ __forceinline__ int cov2_sign(float Vx, uint32_t Sx, float Vy, uint32
 // MEAN ff1, COV af1, MEAN e), compiled in; otherwise the objectives come from
 // the arguments (finish_config, bote_fast.hpp).
 template <int N, bool DEF>
-__global__ void __launch_bounds__(FAST_BD, 4) sweep_group_kernel(FastArgs a) {
+__global__ void __launch_bounds__(FAST_BD, BOTE_GROUP_WAVES) sweep_group_kernel(FastArgs a) {
   using QC = QCfg<N>;
   using GC = GCfg<N>;
   constexpr int NL = QC::NL;
@@ -238,7 +243,7 @@ __global__ void __launch_bounds__(FAST_BD, 4) sweep_group_kernel(FastArgs a) {
   uint32_t* cs1 = (uint32_t*)(smem + off[4]);
   uint64_t* cs2 = (uint64_t*)(smem + off[5]);
   double* vcol = (double*)(smem + off[6]);
-  uint64_t* binom = (uint64_t*)(smem + off[7]);
+  const uint64_t* binom = a.binom;
   TopkLds tk;
   tk.top = (Rec*)(smem + off[9]);
   tk.cand = (Rec*)(smem + off[10]);
@@ -262,7 +267,6 @@ __global__ void __launch_bounds__(FAST_BD, 4) sweep_group_kernel(FastArgs a) {
     }
   }
   for (uint32_t i = tid; i < a.ns; i += FAST_BD) srv[i] = a.srv[i];
-  for (uint32_t i = tid; i < (a.ns + 1) * (N + 1); i += FAST_BD) binom[i] = a.binom[i];
   for (uint32_t i = tid; i < (uint32_t)a.n_obj * KP; i += FAST_BD) tk.top[i] = rec_max();
   if (tid < MAXOBJ) tk.thr[tid] = rec_max();
   if (tid == 0) *lock = 0;
@@ -439,7 +443,7 @@ __global__ void __launch_bounds__(FAST_BD, 4) sweep_group_kernel(FastArgs a) {
             }
 #pragma unroll
             for (int k = N - 1; k < PV; ++k) v[k] = 0xFFFFFFFFu;
-            sort_network_pk<PV>(v);
+            if (!(a.ablate & 32)) sort_network_pk<PV>(v);
             emit_pk(0, true, v);
           }
           {
@@ -450,7 +454,7 @@ __global__ void __launch_bounds__(FAST_BD, 4) sweep_group_kernel(FastArgs a) {
             for (int k = 0; k < F; ++k) v[2 + k] = l16(rqt + freg[k] * rstride + 2 * rv[2]) >> LAT_SHIFT;
 #pragma unroll
             for (int k = N - 1; k < PV; ++k) v[k] = 0xFFFFu;
-            sort_network<PV>(v);
+            if (!(a.ablate & 32)) sort_network<PV>(v);
             emit_pk(2, false, v);
           }
           // ---- fixed rows (pairs): insert the 3 lane distances into the
@@ -463,6 +467,7 @@ __global__ void __launch_bounds__(FAST_BD, 4) sweep_group_kernel(FastArgs a) {
             const bool has_hi = 2 * pp + 1 < F;
 #pragma unroll
             for (int m = 0; m < 3; ++m) {
+              if (a.ablate & 64) break;
               const uint32_t lo = l16(cv[m] + 2 * freg[2 * pp]);
               const uint32_t hi = has_hi ? l16(cv[m] + 2 * freg[has_hi ? 2 * pp + 1 : 2 * pp]) : 0xFFF0u;
               us2 x = as_us2((lo | (hi << 16)) >> LAT_SHIFT);
@@ -487,6 +492,7 @@ __global__ void __launch_bounds__(FAST_BD, 4) sweep_group_kernel(FastArgs a) {
           float bV = vf_of(0);
 #pragma unroll
           for (int l = 1; l < N; ++l) {
+            if (a.ablate & 128) break;
             const uint32_t S = s1_of(l) + nc * Q2[l];
             const float V = vf_of(l);
             if (V == 0.0f && bV == 0.0f) continue;  // both COV exactly 0: keep the first
@@ -605,6 +611,7 @@ __global__ void __launch_bounds__(FAST_BD, 4) sweep_group_kernel(FastArgs a) {
               uint32_t f1 = 0, f1s = 0, f2 = 0, f2s = 0;
 #pragma unroll
               for (int k = 0; k < N; ++k) {
+                if (a.ablate & 512) break;
                 const uint32_t v = l16(lcol + 2 * reg_of(k)) >> LAT_SHIFT;
                 const uint32_t x1 = v + lq2, x2 = v + lq3;
                 f1 += x1;
@@ -625,7 +632,7 @@ __global__ void __launch_bounds__(FAST_BD, 4) sweep_group_kernel(FastArgs a) {
               bool valid = false;
               const int fcap = min(N / 2, a.ft_metric);
               bool defer = false;
-              if (a.want_score) {
+              if (a.want_score && !(a.ablate & 256)) {
                 valid = true;
 #pragma unroll
                 for (int f = 1; f <= 2; ++f) {

@@ -101,7 +101,9 @@ struct FastArgs {
   unsigned long long* queue_count;
   uint64_t queue_cap;
   // timing diagnostics only (env BOTE_ABLATE; results are wrong when set):
-  // 1 skip client loop, 2 skip Q phase, 4 skip top-K step, 8 skip score, 16 skip digest
+  // 1 skip client loop, 2 skip Q phase, 4 skip top-K step, 8 skip score, 16 skip digest;
+  // group kernel: 32 skip variable-row sorts, 64 skip fixed-row insertions,
+  // 128 skip leader selection, 256 skip validity, 512 skip colocated FPaxos
   uint32_t ablate;
 };
 size_t fast_smem_bytes(const FastArgs& a, uint32_t n);
