@@ -592,6 +592,8 @@ int bote_sweep_create(const bote_planet* p, const uint32_t* servers, uint32_t ns
     f.ft_metric = a.ft_metric;
     auto integral = [](double x) { return x == (double)(int64_t)x && x > -1e12 && x < 1e12; };
     f.p_int = integral(a.p_fmean) && integral(a.p_emean) ? 1 : 0;
+    f.p1i = f.p_int ? (int64_t)a.p_fmean * (int64_t)nc : 0;
+    f.p2i = f.p_int ? (int64_t)a.p_emean * (int64_t)nc : 0;
     f.n_obj = a.n_obj;
     for (int o = 0; o < bote::MAXOBJ; ++o) {
       f.obj_kind[o] = a.obj_kind[o];

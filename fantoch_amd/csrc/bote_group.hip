@@ -124,6 +124,13 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
+__device__ __forceinline__ us2 ld_pair(uint32_t a, uint32_t b) {
+  us2 r;
+  r.x = *(const AS3 unsigned short*)(uintptr_t)a;
+  r.y = *(const AS3 unsigned short*)(uintptr_t)b;
+  return r;
+}
+
 __device__ __forceinline__ us2 pk_min(us2 a, us2 b) { return __builtin_elementwise_min(a, b); }
 __device__ __forceinline__ us2 pk_max(us2 a, us2 b) { return __builtin_elementwise_max(a, b); }
 
@@ -486,24 +493,50 @@ __global__ void __launch_bounds__(FAST_BD, BOTE_GROUP_WAVES) sweep_group_kernel(
           auto reg_of = [&](int l) { return l < 3 ? rv[l] : freg[l - 3]; };
           auto s1_of = [&](int l) { return l < 3 ? cs1[pv[l]] : l32(fS1 + 4 * (l - 3)); };
           auto vf_of = [&](int l) { return l < 3 ? (float)vcol[pv[l]] : lf32(fVf + 4 * (l - 3)); };
-          uint32_t bi = 0, bpos = pv[0];
+          // COV^2 proxy r = V / S^2 per member in f32 (V one rounding, S
+          // exact below 2^24, S^2 and the reciprocal one each): within 2^-22
+          // of exact, so comparisons outside a 2^-18 band are decided; any
+          // closer call re-runs the scan exactly (cov2_sign) or defers.
+          uint32_t bi = 0;
           bool amb = false;
-          uint32_t bS = s1_of(0) + nc * Q2[0];
-          float bV = vf_of(0);
+          if (!(a.ablate & 128)) {
+            float rl[N];
 #pragma unroll
-          for (int l = 1; l < N; ++l) {
-            if (a.ablate & 128) break;
-            const uint32_t S = s1_of(l) + nc * Q2[l];
-            const float V = vf_of(l);
-            if (V == 0.0f && bV == 0.0f) continue;  // both COV exactly 0: keep the first
-            const uint32_t pl = pos_of(l);
-            const int c = cov2_sign(V, S, bV, bS, [&] { return vcol[pl]; }, [&] { return vcol[bpos]; });
-            if (c == 0) amb = true;
-            if (c < 0) {
-              bi = l;
-              bS = S;
-              bV = V;
-              bpos = pl;
+            for (int l = 0; l < N; ++l) {
+              const float fs = (float)(s1_of(l) + nc * Q2[l]);
+              rl[l] = vf_of(l) * __builtin_amdgcn_rcpf(fs * fs);
+            }
+            float rb = rl[0];
+#pragma unroll
+            for (int l = 1; l < N; ++l) {
+              const float r = rl[l];
+              const bool lt = r < rb * (1.0f - 0x1p-18f);
+              const bool near = !lt && r <= rb * (1.0f + 0x1p-18f) && (r > 0.0f || rb > 0.0f);
+              amb = amb || near;
+              bi = lt ? (uint32_t)l : bi;
+              rb = lt ? r : rb;
+            }
+          }
+          if (amb) {  // exact re-scan in the generic path's arithmetic
+            amb = false;
+            bi = 0;
+            uint32_t bpos = pv[0];
+            uint32_t bS = s1_of(0) + nc * Q2[0];
+            float bV = vf_of(0);
+#pragma unroll
+            for (int l = 1; l < N; ++l) {
+              const uint32_t S = s1_of(l) + nc * Q2[l];
+              const float V = vf_of(l);
+              if (V == 0.0f && bV == 0.0f) continue;  // both COV exactly 0: keep the first
+              const uint32_t pl = pos_of(l);
+              const int c = cov2_sign(V, S, bV, bS, [&] { return vcol[pl]; }, [&] { return vcol[bpos]; });
+              if (c == 0) amb = true;
+              if (c < 0) {
+                bi = l;
+                bS = S;
+                bV = V;
+                bpos = pl;
+              }
             }
           }
           if (amb) {
@@ -534,27 +567,26 @@ __global__ void __launch_bounds__(FAST_BD, BOTE_GROUP_WAVES) sweep_group_kernel(
                 s2[t] = 0;
               }
               const uint32_t c0 = cqt + rv[0] * cstride, c1 = cqt + rv[1] * cstride, c2 = cqt + rv[2] * cstride;
+              // (m << GQSH) + qlane in one instruction (the compiler would
+              // otherwise re-associate it into shift, and, add)
+              auto qaddr = [&](uint32_t m) {
+                uint32_t r;
+                asm("v_lshl_add_u32 %0, %1, 10, %2" : "=v"(r) : "v"(m), "v"(qlane));
+                return r;
+              };
               auto quad = [&](uint32_t g8, uint32_t mlo, uint32_t mhi) {
                 const uint2 wa = l64(c0 + g8), wb = l64(c1 + g8), wc = l64(c2 + g8), wf = l64(mfl + g8);
                 const us2 lo = pk_min(pk_min(as_us2(wa.x), as_us2(wb.x) | J1), pk_min(as_us2(wc.x) | J2, as_us2(wf.x)));
                 const us2 hi = pk_min(pk_min(as_us2(wa.y), as_us2(wb.y) | J1), pk_min(as_us2(wc.y) | J2, as_us2(wf.y)));
                 const uint32_t L = as_u32(lo), H = as_u32(hi);
-                constexpr int NQ = NL == 3 ? 8 : 4;
-                uint32_t q[NQ];
-                q[0] = l32(qlane + ((L & 15u) << GQSH));
-                q[1] = l32(qlane + (((L >> 16) & 15u) << GQSH));
-                q[2] = l32(qlane + ((H & 15u) << GQSH));
-                q[3] = l32(qlane + (((H >> 16) & 15u) << GQSH));
-                if (NL == 3) {
-                  const uint32_t P2 = qlane + ((uint32_t)N << GQSH);
-                  q[NQ - 4] = l32(P2 + ((L & 15u) << GQSH));
-                  q[NQ - 3] = l32(P2 + (((L >> 16) & 15u) << GQSH));
-                  q[NQ - 2] = l32(P2 + ((H & 15u) << GQSH));
-                  q[NQ - 1] = l32(P2 + (((H >> 16) & 15u) << GQSH));
-                }
+                // qtab address of each client's nearest member: one bitfield
+                // extract + one v_lshl_add per client; the two tables are the
+                // halves of the member's word, read straight into packed pairs
+                const uint32_t a0 = qaddr(L & 15u), a1 = qaddr(__builtin_amdgcn_ubfe(L, 16, 4));
+                const uint32_t a2 = qaddr(H & 15u), a3 = qaddr(__builtin_amdgcn_ubfe(H, 16, 4));
                 const us2 dlo = lo >> (us2)4, dhi = hi >> (us2)4;
-                auto acc1 = [&](int t, uint32_t ql01, uint32_t ql23) {
-                  us2 a01 = dlo + as_us2(ql01), a23 = dhi + as_us2(ql23);
+                auto acc1 = [&](int t, us2 q01, us2 q23) {
+                  us2 a01 = dlo + q01, a23 = dhi + q23;
                   a01 = as_us2(as_u32(a01) & mlo);
                   a23 = as_us2(as_u32(a23) & mhi);
                   S1[t] = __builtin_amdgcn_udot2(a01, ones, S1[t], false);
@@ -562,13 +594,19 @@ __global__ void __launch_bounds__(FAST_BD, BOTE_GROUP_WAVES) sweep_group_kernel(
                   s2[t] = __builtin_amdgcn_udot2(a01, a01, s2[t], false);
                   s2[t] = __builtin_amdgcn_udot2(a23, a23, s2[t], false);
                 };
-                acc1(0, __builtin_amdgcn_perm(q[1], q[0], 0x05040100u), __builtin_amdgcn_perm(q[3], q[2], 0x05040100u));
+                // (16-bit loads into packed halves would need d16 loads, which
+                //  gfx950 with sramecc does not preserve; read words and perm)
+                const uint32_t w0 = l32(a0), w1 = l32(a1), w2 = l32(a2), w3 = l32(a3);
+                acc1(0, as_us2(__builtin_amdgcn_perm(w1, w0, 0x05040100u)), as_us2(__builtin_amdgcn_perm(w3, w2, 0x05040100u)));
                 if (NL >= 2)
-                  acc1(NL >= 2 ? 1 : 0, __builtin_amdgcn_perm(q[1], q[0], 0x07060302u),
-                       __builtin_amdgcn_perm(q[3], q[2], 0x07060302u));
-                if (NL == 3)
-                  acc1(NL - 1, __builtin_amdgcn_perm(q[NQ - 3], q[NQ - 4], 0x05040100u),
-                       __builtin_amdgcn_perm(q[NQ - 1], q[NQ - 2], 0x05040100u));
+                  acc1(NL >= 2 ? 1 : 0, as_us2(__builtin_amdgcn_perm(w1, w0, 0x07060302u)),
+                       as_us2(__builtin_amdgcn_perm(w3, w2, 0x07060302u)));
+                if (NL == 3) {
+                  constexpr uint32_t P2 = (uint32_t)N << GQSH;
+                  const uint32_t x0 = l32(a0 + P2), x1 = l32(a1 + P2), x2 = l32(a2 + P2), x3 = l32(a3 + P2);
+                  acc1(NL - 1, as_us2(__builtin_amdgcn_perm(x1, x0, 0x05040100u)),
+                       as_us2(__builtin_amdgcn_perm(x3, x2, 0x05040100u)));
+                }
               };
               auto flush = [&]() {
 #pragma unroll
@@ -578,11 +616,29 @@ __global__ void __launch_bounds__(FAST_BD, BOTE_GROUP_WAVES) sweep_group_kernel(
                 }
               };
               const uint32_t nql = (a.ablate & 1) ? 0u : nq;
-              for (uint32_t g0 = 0; g0 < nql; g0 += a.s2_flush) {
-                const uint32_t ge = min(nql, g0 + a.s2_flush);
-#pragma unroll 4
-                for (uint32_t g = g0; g < ge; ++g) quad(g * 8, ~0u, ~0u);
-                flush();
+              // 4 quads per iteration (constant offsets fold into the ds_read
+              // offset fields); s2 is flushed to 64 bits every s2_flush quads
+              {
+                const uint32_t f4 = a.s2_flush >> 2 ? a.s2_flush >> 2 : 1u;
+                uint32_t g = 0, k = 0;
+                if (a.s2_flush >= 4) {
+                  for (; g + 4 <= nql; g += 4) {
+                    quad(g * 8, ~0u, ~0u);
+                    quad(g * 8 + 8, ~0u, ~0u);
+                    quad(g * 8 + 16, ~0u, ~0u);
+                    quad(g * 8 + 24, ~0u, ~0u);
+                    if (++k == f4) {
+                      flush();
+                      k = 0;
+                    }
+                  }
+                  flush();
+                }
+                for (uint32_t g0 = g; g0 < nql; g0 += a.s2_flush) {
+                  const uint32_t ge = min(nql, g0 + a.s2_flush);
+                  for (g = g0; g < ge; ++g) quad(g * 8, ~0u, ~0u);
+                  flush();
+                }
               }
               if (rem && !(a.ablate & 1)) {
                 quad(nq * 8, rem >= 2 ? ~0u : 0x0000FFFFu, rem == 3 ? 0x0000FFFFu : 0u);
@@ -608,17 +664,17 @@ __global__ void __launch_bounds__(FAST_BD, BOTE_GROUP_WAVES) sweep_group_kernel(
             //      submatrix; leaderless values are the members' own quorums
             {
               const uint32_t lcol = rqt + lreg * rstride;
-              uint32_t f1 = 0, f1s = 0, f2 = 0, f2s = 0;
+              // sum_k (v_k + q) and sum_k (v_k + q)^2 from sum v and sum v^2
+              uint32_t sv = 0, sv2 = 0;
 #pragma unroll
               for (int k = 0; k < N; ++k) {
                 if (a.ablate & 512) break;
                 const uint32_t v = l16(lcol + 2 * reg_of(k)) >> LAT_SHIFT;
-                const uint32_t x1 = v + lq2, x2 = v + lq3;
-                f1 += x1;
-                f1s += x1 * x1;
-                f2 += x2;
-                f2s += x2 * x2;
+                sv += v;
+                sv2 += v * v;
               }
+              const uint32_t f1 = sv + N * lq2, f2 = sv + N * lq3;
+              const uint32_t f1s = sv2 + 2 * lq2 * sv + N * lq2 * lq2, f2s = sv2 + 2 * lq3 * sv + N * lq3 * lq3;
               mom[5 + SLOT_FF1] = Mom{f1, f1s, (uint32_t)N};
               mom[5 + SLOT_FF2] = Mom{f2, f2s, (uint32_t)N};
               const uint32_t cl1[3] = {cS1p & 0xFFFFu, cS1p >> 16, cS1e};
@@ -627,6 +683,8 @@ __global__ void __launch_bounds__(FAST_BD, BOTE_GROUP_WAVES) sweep_group_kernel(
               mom[5 + SLOT_E] = Mom{cl1[QC::idx_e], cS2[QC::idx_e], (uint32_t)N};
             }
             const double vlead = vcol[lpos];
+            const float vlead32 = (float)vlead;
+            float r_af1 = -1.0f;  // af1's V / S^2 when the validity scan computed it
             if (DEF) {
               // ---- compute_score validity (search.rs:421-472), exact
               bool valid = false;
@@ -642,15 +700,21 @@ __global__ void __launch_bounds__(FAST_BD, BOTE_GROUP_WAVES) sweep_group_kernel(
                   // fmi >= p1: integers unless the sums meet exactly
                   const int64_t D = (int64_t)mf.s1 - (int64_t)ma.s1;
                   bool mok;
-                  if (a.p_int && (double)D != pnc1) mok = (double)D > pnc1;
+                  if (a.p_int && D != a.p1i) mok = D > a.p1i;
                   else mok = (mom_mean(mf) - mom_mean(ma)) >= a.p_fmean;
                   valid = valid && mok;
                   if (valid) {
                     // cov_f >= cov_a (min_fairness_fpaxos_improv == 0 on this path)
                     const uint64_t Va = mom_v(ma);
                     if (!(vlead == 0.0 && Va == 0)) {
-                      const int c = cov2_sign((float)vlead, (uint32_t)mf.s1, (float)Va, (uint32_t)ma.s1,
-                                              [&] { return vlead; }, [&] { return (double)Va; });
+                      const float sf = (float)(uint32_t)mf.s1, sa = (float)(uint32_t)ma.s1;
+                      const float rf = vlead32 * __builtin_amdgcn_rcpf(sf * sf);
+                      const float ra = (float)Va * __builtin_amdgcn_rcpf(sa * sa);
+                      if (f == 1) r_af1 = ra;
+                      int c = rf > ra * (1.0f + 0x1p-18f) ? 1 : (rf < ra * (1.0f - 0x1p-18f) ? -1 : 0);
+                      if (c == 0)
+                        c = cov2_sign(vlead32, (uint32_t)mf.s1, (float)Va, (uint32_t)ma.s1, [&] { return vlead; },
+                                      [&] { return (double)Va; });
                       if (c == 0) defer = true;
                       valid = valid && c > 0;
                     }
@@ -658,7 +722,7 @@ __global__ void __launch_bounds__(FAST_BD, BOTE_GROUP_WAVES) sweep_group_kernel(
                   if (N == 11 || N == 13) {
                     const int64_t De = (int64_t)mom[SLOT_E].s1 - (int64_t)ma.s1;
                     bool eok;
-                    if (a.p_int && (double)De != pnc2) eok = (double)De > pnc2;
+                    if (a.p_int && De != a.p2i) eok = De > a.p2i;
                     else eok = (mom_mean(mom[SLOT_E]) - mom_mean(ma)) >= a.p_emean;
                     valid = valid && eok;
                   }
@@ -715,11 +779,16 @@ __global__ void __launch_bounds__(FAST_BD, BOTE_GROUP_WAVES) sweep_group_kernel(
                 {
                   const Mom& m = mom[SLOT_AF1];
                   const uint64_t tk3 = tk.thr[3].key;
-                  const uint64_t V = mom_v(m);
                   // f32 screen with a 2^-10 margin (conservative: offers a superset)
-                  const float S = (float)m.s1;
-                  const bool maybe = tk3 == ~0ull ||
-                                     (float)V <= (float)__longlong_as_double((long long)tk3) * (S * S) * (1.0f + 0x1p-10f);
+                  bool maybe = tk3 == ~0ull;
+                  if (!maybe) {
+                    float r = r_af1;
+                    if (r < 0.0f) {
+                      const float S = (float)(uint32_t)m.s1;
+                      r = (float)mom_v(m) * __builtin_amdgcn_rcpf(S * S);
+                    }
+                    maybe = r <= (float)__longlong_as_double((long long)tk3) * (1.0f + 0x1p-10f);
+                  }
                   if (maybe) {
                     ok[3] = true;
                     key[3] = cov_key(m);

@@ -85,6 +85,7 @@ struct FastArgs {
   uint32_t runlen;
   uint32_t s2_flush;  // quads per 32-bit sum-of-squares chunk
   int want_score, p_int;
+  int64_t p1i, p2i;  // p_int: min_mean_{fpaxos,epaxos}_improv * nc as integers
   double p_fmean, p_emean;
   int ft_metric;
   int n_obj;

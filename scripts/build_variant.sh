@@ -1,0 +1,15 @@
+#!/bin/bash
+# Build an A/B variant of libbote_hip.so with extra compiler flags:
+#   scripts/build_variant.sh NAME "-DFOO=1"   ->  fantoch_amd/lib_NAME/libbote_hip.so
+# Use it with BOTE_LIB_PATH=fantoch_amd/lib_NAME/libbote_hip.so (timing experiments only).
+set -e
+NAME=$1; FLAGS=$2
+D=fantoch_amd/lib_$NAME
+mkdir -p $D/obj
+H="/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -Wno-unused-result $FLAGS"
+for f in bote_kernels bote_sweep bote_group bote_capi; do
+  if [ "$f" = bote_group ] || [ ! -f $D/obj/$f.o ]; then $H -c fantoch_amd/csrc/$f.hip -o $D/obj/$f.o & fi
+done
+wait
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $D/libbote_hip.so $D/obj/*.o
+echo built $D/libbote_hip.so
