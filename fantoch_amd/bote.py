@@ -19,7 +19,7 @@ from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 
-from . import _lib
+from . import _lib, bincode
 from ._lib import check, lib, ptr, u32
 from .metrics import F64, Histogram, Stats
 from .planet import Planet, Region
@@ -250,6 +250,34 @@ class ConfigAndStats:
         yield self.stats
 
 
+def _slot_key(slot: int) -> str:
+    proto, f = SLOT_KEYS[slot % 5]
+    return ProtocolStats.key(proto, f, ClientPlacement.Input if slot < 5 else ClientPlacement.Colocated)
+
+
+class _DeviceConfigStats:
+    """The `Vec<(BTreeSet<Region>, ProtocolStats)>` of one n, produced lazily in
+    device batches (bote_eval with per-client outputs) for the bincode writer."""
+
+    def __init__(self, search: "Search", ci: int, n: int):
+        self.s, self.ci, self.n = search, ci, n
+        self.d = search.all_configs[ci][1][n]
+
+    def __len__(self):
+        return len(self.d["cfg"])
+
+    def __iter__(self):
+        d, n, names = self.d, self.n, self.s.planet.names
+        slots = [s for s in range(10) if not (SLOT_KEYS[s % 5][0] is not Protocol.EPaxos and
+                                                SLOT_KEYS[s % 5][1] > max_f(n))]
+        for b in range(0, len(d["cfg"]), Search.BATCH):
+            cfg = d["cfg"][b:b + Search.BATCH]
+            r = eval_configs(self.s.dp, d["srv"], d["cli"], n, configs=cfg)
+            for i in range(len(cfg)):
+                stats = {_slot_key(s): bincode.histogram_pairs(r.slot_values(i, s)) for s in slots}
+                yield [names[d["srv"][p]] for p in cfg[i]], stats
+
+
 class Search:
     """search.rs:41-512 — exhaustive search, computed on the GPU."""
 
@@ -263,6 +291,7 @@ class Search:
         filename = self.filename(min_n, max_n, search_input)
         servers, all_clients = search_input.get_inputs(max_n, self.planet)
         self.all_configs: List[Tuple[List[Region], Dict[int, dict]]] = []
+        self._file_stats: Dict[Tuple[int, int, int], dict] = {}
         loaded = self._load(filename) if os.path.exists(filename) else None
         if loaded is not None:
             self.all_configs = loaded
@@ -276,8 +305,8 @@ class Search:
 
     @staticmethod
     def filename(min_n: int, max_n: int, search_input: SearchInput) -> str:
-        """search.rs:479-485 (stored as .npz instead of bincode)."""
-        return f"{min_n}_{max_n}_{search_input}.npz"
+        """search.rs:479-485 — the reference's bincode cache name."""
+        return f"{min_n}_{max_n}_{search_input}.data"
 
     # search.rs:234-260 — configs of each n in lexicographic order of positions.
     def _compute_configs(self, min_n: int, max_n: int, servers: Sequence[Region], clients: Sequence[Region]):
@@ -301,31 +330,62 @@ class Search:
         return out
 
     def _save(self, filename: str):
-        arrs = {}
-        for ci, (clients, configs) in enumerate(self.all_configs):
-            arrs[f"c{ci}_clients"] = self.planet.idxs(clients)
-            for n, d in configs.items():
-                for k, v in d.items():
-                    arrs[f"c{ci}_n{n}_{k}"] = v
-        np.savez(filename, **arrs)
+        """search.rs:500-512: bincode `Search` (fantoch_amd/bincode.py), full per-config
+        histograms from the device (bote_eval with per-client outputs)."""
+        with open(filename, "wb") as w:
+            bincode.write_search(w, [([r.name for r in clients], {n: _DeviceConfigStats(self, ci, n)
+                                                                   for n in configs})
+                                     for ci, (clients, configs) in enumerate(self.all_configs)])
+
+    def save_data(self, filename: Optional[str] = None) -> str:
+        """Write this search as the reference's `.data` file; returns its path."""
+        filename = filename or self.filename(self.min_n, self.max_n, self.search_input)
+        self._save(filename)
+        return filename
 
     def _load(self, filename: str):
-        z = np.load(filename, allow_pickle=False)
+        """search.rs:487-498: read a bincode `Search` (written by the Rust crate or by
+        `_save`).  Its histograms are kept as the configs' stats; per-key means,
+        sums and COVs are derived from them (Histogram::mean / cov)."""
+        with open(filename, "rb") as fh:
+            data = bincode.read_search(fh.read())
+        servers, _ = self.search_input.get_inputs(self.max_n, self.planet)
         out = []
-        ci = 0
-        while f"c{ci}_clients" in z:
-            clients = [Region(self.planet.names[i]) for i in z[f"c{ci}_clients"]]
-            configs = {}
-            for n in range(self.min_n, self.max_n + 1, 2):
-                d = {k: z[f"c{ci}_n{n}_{k}"] for k in ("cfg", "mean", "s1", "cov", "srv", "cli")
-                     if f"c{ci}_n{n}_{k}" in z}
-                configs[n] = d
-            out.append((clients, configs))
-            ci += 1
+        for ci, (client_names, configs) in enumerate(data):
+            clients = [Region(x) for x in client_names]
+            cli_ids = self.planet.idxs(clients)
+            srv_ids = self.planet.idxs(servers if servers is not None else clients)
+            pos_of = {int(r): p for p, r in enumerate(srv_ids)}
+            name_id = {nm: i for i, nm in enumerate(self.planet.names)}
+            per_n = {}
+            for n, lst in configs.items():
+                cfg = np.zeros((len(lst), n), np.uint32)
+                s1 = np.zeros((len(lst), 10), np.uint64)
+                mean = np.zeros((len(lst), 10))
+                cov = np.zeros((len(lst), 10))
+                for i, (names, stats) in enumerate(lst):
+                    if len(names) != n:
+                        raise ValueError(f"{filename}: config of size {len(names)} under n={n}")
+                    # servers-list order = the order the reference's combination() yields
+                    cfg[i] = sorted(pos_of[name_id[x]] for x in names)
+                    self._file_stats[(ci, n, i)] = stats
+                    for slot in range(10):
+                        k = _slot_key(slot)
+                        if k in stats:
+                            h = Histogram({int(v): int(c) for v, c in stats[k]})
+                            s1[i, slot] = sum(int(v) * int(c) for v, c in stats[k])
+                            mean[i, slot] = h.mean().value()
+                            cov[i, slot] = h.cov().value()
+                per_n[n] = dict(cfg=cfg, mean=mean, s1=s1, cov=cov, srv=srv_ids, cli=cli_ids)
+            out.append((clients, per_n))
         return out
 
     def _stats(self, ci: int, n: int, i: int) -> ProtocolStats:
         key = (ci, n, i)
+        if key not in self._stats_cache and key in self._file_stats:
+            st = ProtocolStats.new()
+            st.map = {k: Histogram({int(v): int(c) for v, c in h}) for k, h in self._file_stats[key].items()}
+            self._stats_cache[key] = st
         if key not in self._stats_cache:
             d = self.all_configs[ci][1][n]
             r = eval_configs(self.dp, d["srv"], d["cli"], n, configs=d["cfg"][i:i + 1])

@@ -64,6 +64,25 @@ def test_best_latency_leader(bote):
     assert (h.mean().round(), h.cov().round(), h.mdtm().round()) == (g["mean"], g["cov"], g["mdtm"])
 
 
+def test_tempo_fast_quorums_leaderless(gcp, bote):
+    """BASELINE config 2's Tempo: fast quorums n/2+f and, tiny, 2f
+    (fantoch/src/config.rs:317-329) through Bote::leaderless (lib.rs:38-59)."""
+    p, _, o = gcp
+    rng = np.random.default_rng(7)
+    for n in (3, 5, 7, 9, 13):
+        for f in range(1, min(n // 2, 2) + 1):
+            for tiny, proto in ((False, _lib.TEMPO), (True, _lib.TEMPO_TINY)):
+                q = _lib.lib().bote_quorum_size(proto, n, f)
+                assert q == (2 * f if tiny else n // 2 + f)
+                for _ in range(4):
+                    srv = rng.choice(p.R, n, replace=False)
+                    cli = rng.choice(p.R, 11, replace=False)
+                    got = bote.leaderless([p.names[i] for i in srv], [p.names[i] for i in cli], q)
+                    want = o.leaderless(srv, cli, q)
+                    assert [r.name for r, _ in got] == [p.names[i] for i in cli]
+                    assert [v for _, v in got] == want.tolist()
+
+
 def test_single_config_api_vs_oracle(gcp):
     p, dp, o = gcp
     b = Bote(p)
