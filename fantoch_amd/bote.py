@@ -360,9 +360,11 @@ class Search:
             per_n = {}
             for n, lst in configs.items():
                 cfg = np.zeros((len(lst), n), np.uint32)
-                s1 = np.zeros((len(lst), 10), np.uint64)
-                mean = np.zeros((len(lst), 10))
-                cov = np.zeros((len(lst), 10))
+                # slots a config does not have (f=2 at n<4): sums all-ones, mean/COV NaN,
+                # as bote_eval leaves them
+                s1 = np.full((len(lst), 10), np.iinfo(np.uint64).max, np.uint64)
+                mean = np.full((len(lst), 10), np.nan)
+                cov = np.full((len(lst), 10), np.nan)
                 for i, (names, stats) in enumerate(lst):
                     if len(names) != n:
                         raise ValueError(f"{filename}: config of size {len(names)} under n={n}")
