@@ -148,7 +148,7 @@ def main():
         traffic = load_traffic(f"{args.workload}_n{world}")
         grid, block, lds = sweep.geometry()
         out = {
-            "metric": METRIC,
+            "metric": METRIC if args.workload == "r64n7" else f"region configs evaluated/sec, {wl['desc']}",
             "value": total * args.steps / dt,
             "unit": "configs/s",
             "n_gpus": world,
