@@ -636,7 +636,7 @@ int eval_occupancy(uint32_t n, bool full, uint32_t bd, size_t shm) {
 #undef OCC_CASE
     default: return 0;
   }
-  hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
+  if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm) != hipSuccess) return 1;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, (int)bd, shm) != hipSuccess) return 1;
   return nb > 0 ? nb : 1;
 }
