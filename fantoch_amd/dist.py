@@ -43,6 +43,15 @@ def sharded_sweep(sweep, stream=None, group=None, device: str = "cuda"):
         return sweep.parse_block(blk.cpu().numpy())
     gathered = torch.empty(world * nbytes, dtype=torch.uint8, device=device)
     dist.all_gather_into_tensor(gathered, blk, group=group)
+    return merge_gathered(sweep, gathered, world, stream, device)
+
+
+def merge_gathered(sweep, gathered, world: int, stream=None, device: str = "cuda"):
+    """Deterministic merge of `world` concatenated result blocks (the all-gather
+    output, rank order) into one result; every rank runs it on its own copy."""
+    import torch
+
+    nbytes = sweep.result_bytes()
     out = torch.empty(nbytes, dtype=torch.uint8, device=device)
     # merge_device takes at most 8 blocks per call: a tree for larger worlds
     src, n = gathered, world

@@ -448,3 +448,28 @@ def test_fast_path_deferral_overflow():
         got = _sweep(dp, srv, srv, 5, 0, total, kernel=k)
         assert (got.valid, got.digest) == (valid, digest)
         assert got.tops == [list(t) for t in tops]
+
+
+@pytest.mark.parametrize("world", [2, 8, 9])
+def test_sharded_merge_tree_on_device(gcp, world):
+    """bench.py's N>1 data path minus RCCL: `world` contiguous shards swept on
+    the device, their result blocks concatenated in rank order (what
+    all_gather_into_tensor yields) and merged by dist.merge_gathered (a tree
+    beyond 8 shards) equal one unsharded sweep."""
+    import torch
+
+    from fantoch_amd.dist import merge_gathered, shard_range
+
+    p, dp, _ = gcp
+    srv = np.arange(p.R, dtype=np.uint32)
+    sw = Sweep(dp, srv, srv, 7, DEFAULT_OBJECTIVES, K=100, ranking=DEFAULT_RANKING, digest=True)
+    sw.launch(0, sw.total)
+    full = sw.result()
+    nb = sw.result_bytes()
+    gathered = torch.empty(world * nb, dtype=torch.uint8, device="cuda")
+    for r in range(world):
+        b, e = shard_range(sw.total, world, r)
+        sw.launch(b, e)
+        sw.result_device(gathered.data_ptr() + r * nb)
+    merged = merge_gathered(sw, gathered, world)
+    assert merged.tops == full.tops and merged.valid == full.valid and merged.digest == full.digest
