@@ -498,17 +498,41 @@ __global__ void __launch_bounds__(256) eval_kernel(EvalArgs a) {
 // ----------------------------------------------------- top-K list merge --
 // lists: n_lists lists, list i of objective o at src[i * list_stride + o * KP]
 // out:   one list per group of G_MERGE_LISTS lists, at dst[g * out_stride + o * KP]
+// Every input list is sorted (block top-K lists, padded with rec_max), so each
+// record's output slot is its rank in the union: its index in its own list
+// plus, per other list, how many records precede it there (ties go to the
+// lower list index).  One pass of binary searches in LDS, no sort; a block
+// that finds an unsorted input falls back to the full bitonic sort.
 __global__ void __launch_bounds__(256) merge_kernel(const Rec* src, uint32_t n_lists, uint64_t list_stride, Rec* dst,
                                                      uint64_t out_stride) {
   __shared__ Rec buf[G_MERGE_LISTS * KP];
+  __shared__ int unsorted;
   const uint32_t g = blockIdx.x, o = blockIdx.y;
+  if (threadIdx.x == 0) unsorted = 0;
   for (uint32_t i = threadIdx.x; i < G_MERGE_LISTS * KP; i += blockDim.x) {
     uint32_t l = g * G_MERGE_LISTS + i / KP;
     buf[i] = l < n_lists ? src[l * list_stride + o * KP + i % KP] : rec_max();
   }
   __syncthreads();
-  block_bitonic(buf, G_MERGE_LISTS * KP);
-  for (uint32_t i = threadIdx.x; i < KP; i += blockDim.x) dst[g * out_stride + o * KP + i] = buf[i];
+  for (uint32_t i = threadIdx.x; i < G_MERGE_LISTS * KP; i += blockDim.x)
+    if (i % KP && rec_lt(buf[i], buf[i - 1])) unsorted = 1;
+  __syncthreads();
+  Rec* out = dst + g * out_stride + o * KP;
+  if (unsorted) {  // block-uniform
+    block_bitonic(buf, G_MERGE_LISTS * KP);
+    for (uint32_t i = threadIdx.x; i < KP; i += blockDim.x) out[i] = buf[i];
+    return;
+  }
+  for (uint32_t i = threadIdx.x; i < G_MERGE_LISTS * KP; i += blockDim.x) {
+    const uint32_t l = i / KP;
+    const Rec x = buf[i];
+    uint32_t pos = i % KP;
+    for (uint32_t m = 0; m < (uint32_t)G_MERGE_LISTS && pos < (uint32_t)KP; ++m) {
+      if (m == l) continue;
+      pos += m < l ? upper_bound_rec(buf + m * KP, KP, x) : lower_bound_rec(buf + m * KP, KP, x);
+    }
+    if (pos < (uint32_t)KP) out[pos] = x;
+  }
 }
 
 // ------------------------------------------------- single-config kernels --
