@@ -547,17 +547,12 @@ class Sweep:
     def parse_block(self, blk: np.ndarray) -> SweepResult:
         """Host view of a device result block (bote_sweep_result_device layout)."""
         no, K = len(self.objectives), self.K
-        b = np.frombuffer(blk.tobytes(), dtype=np.uint64)
-        recs = b[:no * _lib.KP * 2].reshape(no, _lib.KP, 2)
-        tops = []
-        for o in range(no):
-            lst = []
-            for i in range(K):
-                k, r = int(recs[o, i, 0]), int(recs[o, i, 1])
-                if k == 0xFFFFFFFFFFFFFFFF and r == 0xFFFFFFFFFFFFFFFF:
-                    break
-                lst.append((k, r))
-            tops.append(lst)
+        b = np.frombuffer(np.ascontiguousarray(blk), dtype=np.uint64)
+        recs = b[:no * _lib.KP * 2].reshape(no, _lib.KP, 2)[:, :K]
+        # each list ends at its first (all-ones, all-ones) padding record
+        pad = (recs[:, :, 0] == np.uint64(0xFFFFFFFFFFFFFFFF)) & (recs[:, :, 1] == np.uint64(0xFFFFFFFFFFFFFFFF))
+        ends = np.where(pad.any(axis=1), pad.argmax(axis=1), K)
+        tops = [list(map(tuple, recs[o, :ends[o]].tolist())) for o in range(no)]
         return SweepResult(tops, int(b[no * _lib.KP * 2]), int(b[no * _lib.KP * 2 + 1]))
 
     def kernel_ms(self) -> float:
