@@ -520,6 +520,59 @@ class Sweep:
         except Exception:
             pass
 
+    def run_checkpointed(self, path: str, rank_begin: int = 0, rank_end: Optional[int] = None,
+                         chunk: int = 1 << 28, stop_after: Optional[int] = None) -> Optional[SweepResult]:
+        """Resumable sweep of [rank_begin, rank_end) in rank chunks (SURVEY.md §5:
+        the reference only memoises a finished search, search.rs:55-57; a long
+        sweep here checkpoints its running top-K instead).  After each chunk the
+        running result block, merged on the device, and the next rank are
+        written atomically to `path`; a later call with the same sweep and range
+        resumes there.  `stop_after` ends the call after that many chunks and
+        returns None (an interruption, for tests)."""
+        import torch
+
+        re = self.total if rank_end is None else rank_end
+        if not 0 <= rank_begin <= re <= self.total or chunk < 1:
+            raise ValueError("bad rank range or chunk")
+        ident = np.concatenate([np.array([self.n, self.K, rank_begin, re, len(self.servers), len(self.clients)],
+                                         np.uint64), self.servers.astype(np.uint64), self.clients.astype(np.uint64),
+                                np.asarray(self.objectives, np.uint64).reshape(-1),
+                                np.asarray(self.dp.planet.lat, np.uint64).reshape(-1)])
+        dev = torch.device("cuda", self.dp.device)
+        st = torch.cuda.current_stream(dev).cuda_stream
+        nb = self.result_bytes()
+        pair = torch.empty(2 * nb, dtype=torch.uint8, device=dev)
+        out = torch.empty(nb, dtype=torch.uint8, device=dev)
+        nxt, have = rank_begin, False
+        if os.path.exists(path):
+            z = np.load(path, allow_pickle=False)
+            if not np.array_equal(z["ident"], ident):
+                raise ValueError(f"checkpoint {path} belongs to a different sweep")
+            nxt = int(z["next"])
+            pair[:nb].copy_(torch.from_numpy(np.ascontiguousarray(z["block"])))
+            have = True
+        chunks = 0
+        while nxt < re or not have:
+            e = min(re, nxt + chunk)
+            self.launch(nxt, e, st)
+            if have:
+                self.result_device(pair.data_ptr() + nb, st)
+                self.merge_device(pair.data_ptr(), 2, out.data_ptr(), st)
+                pair[:nb].copy_(out)
+            else:
+                self.result_device(pair.data_ptr(), st)
+                have = True
+            nxt = e
+            blk = pair[:nb].cpu().numpy()
+            tmp = path + ".tmp"
+            with open(tmp, "wb") as fh:
+                np.savez(fh, ident=ident, next=np.uint64(nxt), block=blk)
+            os.replace(tmp, path)
+            chunks += 1
+            if stop_after is not None and chunks >= stop_after and nxt < re:
+                return None
+        return self.parse_block(pair[:nb].cpu().numpy())
+
     def launch(self, rank_begin: int = 0, rank_end: Optional[int] = None, stream: Optional[int] = None):
         re = self.total if rank_end is None else rank_end
         check(lib().bote_sweep_launch(self.h, rank_begin, re, C.c_void_p(stream) if stream else None))

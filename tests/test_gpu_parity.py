@@ -473,3 +473,25 @@ def test_sharded_merge_tree_on_device(gcp, world):
         sw.result_device(gathered.data_ptr() + r * nb)
     merged = merge_gathered(sw, gathered, world)
     assert merged.tops == full.tops and merged.valid == full.valid and merged.digest == full.digest
+
+
+def test_checkpointed_sweep_resumes(gcp, tmp_path):
+    """A chunked sweep interrupted after 3 chunks and resumed from its
+    checkpoint equals the one-shot sweep; a checkpoint of another sweep is
+    refused."""
+    p, dp, _ = gcp
+    srv = np.arange(p.R, dtype=np.uint32)
+    sw = Sweep(dp, srv, srv, 7, DEFAULT_OBJECTIVES, K=100, ranking=DEFAULT_RANKING, digest=True)
+    sw.launch(0, sw.total)
+    full = sw.result()
+    ck = str(tmp_path / "sweep.ckpt")
+    assert sw.run_checkpointed(ck, chunk=9000, stop_after=3) is None
+    assert os.path.exists(ck)
+    res = sw.run_checkpointed(ck, chunk=9000)
+    assert res.tops == full.tops and res.valid == full.valid and res.digest == full.digest
+    # a finished checkpoint returns the result without sweeping again
+    again = sw.run_checkpointed(ck, chunk=9000)
+    assert again.tops == full.tops and again.digest == full.digest
+    other = Sweep(dp, srv, srv, 5, DEFAULT_OBJECTIVES, K=100, ranking=DEFAULT_RANKING, digest=True)
+    with pytest.raises(ValueError):
+        other.run_checkpointed(ck)
