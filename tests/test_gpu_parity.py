@@ -12,6 +12,7 @@ import pytest
 
 import oracle as O
 from fantoch_amd import _lib
+from fantoch_amd.bote import SLOT_KEYS as SLOT_KEYS_T
 from fantoch_amd.bote import (DEFAULT_OBJECTIVES, DEFAULT_RANKING, Bote, DevicePlanet, FTMetric, RankingParams,
                               Search, SearchInput, Sweep, eval_configs)
 from fantoch_amd.metrics import Stats
@@ -495,3 +496,31 @@ def test_checkpointed_sweep_resumes(gcp, tmp_path):
     other = Sweep(dp, srv, srv, 5, DEFAULT_OBJECTIVES, K=100, ranking=DEFAULT_RANKING, digest=True)
     with pytest.raises(ValueError):
         other.run_checkpointed(ck)
+
+
+def test_search_r17cmaxn_client_sets(gcp):
+    """search.rs:199-232 with many client sets (R17CMaxN: every max_n-subset of
+    the 17 regions is a client set and its own server list); per-config stats
+    against the oracle for a sample of the sets."""
+    p, _, o = gcp
+    s = Search(3, 5, SearchInput.R17CMaxN, planet=p)
+    assert len(s.all_configs) == math.comb(17, 5)
+    for ci in range(0, len(s.all_configs), 397):
+        clients, configs = s.all_configs[ci]
+        cli = p.idxs(clients)
+        for n in (3, 5):
+            d = configs[n]
+            assert len(d["cfg"]) == math.comb(5, n)
+            for i in range(len(d["cfg"])):
+                ids = np.array([d["srv"][q] for q in d["cfg"][i]], dtype=np.uint32)
+                vals, lead = o.compute_stats(ids.reshape(1, n), cli)
+                st = s._stats(ci, n, i)
+                for slot in range(10):
+                    seg = (vals[0, slot * len(cli):(slot + 1) * len(cli)] if slot < 5
+                           else vals[0, 5 * len(cli) + (slot - 5) * n:5 * len(cli) + (slot - 4) * n])
+                    proto, f = SLOT_KEYS_T[slot % 5]
+                    if f > min(n // 2, 2):
+                        continue
+                    from fantoch_amd.protocol import ClientPlacement
+                    h = st.get(proto, f, ClientPlacement.Input if slot < 5 else ClientPlacement.Colocated)
+                    assert list(h.iter_values()) == sorted(seg.tolist())
