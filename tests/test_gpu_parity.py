@@ -524,3 +524,20 @@ def test_search_r17cmaxn_client_sets(gcp):
                     from fantoch_amd.protocol import ClientPlacement
                     h = st.get(proto, f, ClientPlacement.Input if slot < 5 else ClientPlacement.Colocated)
                     assert list(h.iter_values()) == sorted(seg.tolist())
+
+
+@pytest.mark.parametrize("n", [2, 4, 6, 7, 8, 9, 10, 11, 12])
+def test_gcp_config2_full_sweep_digest(gcp, n):
+    """BASELINE config 2 in full: every GCP R=20 config of size n (odd = the
+    reference's n, even = extension) swept on the device; the digest covers
+    every config's 10 slot moments and FPaxos leader, so equal digests, valid
+    counts and top-K lists mean the whole sweep matches the oracle."""
+    p, dp, o = gcp
+    srv = np.arange(p.R, dtype=np.uint32)
+    rp = RankingParams.new(30, 10, 0, 15, 3, 13, FTMetric.F1F2)
+    sw = Sweep(dp, srv, srv, n, DEFAULT_OBJECTIVES, K=100, ranking=rp, digest=True)
+    sw.launch(0, sw.total)
+    got = sw.result()
+    tops, valid, digest = _oracle_sweep(o, srv, srv, n, 0, sw.total, DEFAULT_OBJECTIVES, 100, rp)
+    assert (got.valid, got.digest) == (valid, digest)
+    assert got.tops == [list(t) for t in tops]
