@@ -541,3 +541,32 @@ def test_gcp_config2_full_sweep_digest(gcp, n):
     tops, valid, digest = _oracle_sweep(o, srv, srv, n, 0, sw.total, DEFAULT_OBJECTIVES, 100, rp)
     assert (got.valid, got.digest) == (valid, digest)
     assert got.tops == [list(t) for t in tops]
+
+
+def test_sweep_full_r128_n6_properties():
+    """BASELINE config 5 in full (5,423,611,200 configs): shard invariance of
+    the merged result and the top records' keys re-derived by the oracle."""
+    import torch
+
+    from fantoch_amd.dist import merge_gathered, shard_range
+
+    p = Planet.synthetic(128)
+    dp = DevicePlanet(p)
+    o = O.OraclePlanet.of(p)
+    srv = np.arange(128, dtype=np.uint32)
+    sw = Sweep(dp, srv, srv, 6, DEFAULT_OBJECTIVES, K=100, ranking=DEFAULT_RANKING, digest=True)
+    assert sw.total == 5423611200
+    sw.launch(0, sw.total)
+    full = sw.result()
+    nb = sw.result_bytes()
+    gathered = torch.empty(3 * nb, dtype=torch.uint8, device="cuda")
+    for r in range(3):
+        b, e = shard_range(sw.total, 3, r)
+        sw.launch(b, e)
+        sw.result_device(gathered.data_ptr() + r * nb)
+    merged = merge_gathered(sw, gathered, 3)
+    assert merged.tops == full.tops and merged.valid == full.valid and merged.digest == full.digest
+    for oi, (kind, slot) in enumerate(DEFAULT_OBJECTIVES):
+        for key, rank in full.tops[oi][:5]:
+            tops, _, _ = _oracle_sweep(o, srv, srv, 6, rank, rank + 1, [(kind, slot)], 1, DEFAULT_RANKING, 1)
+            assert tops[0] == [(key, rank)]
