@@ -357,6 +357,10 @@ class Search:
             srv_ids = self.planet.idxs(servers if servers is not None else clients)
             pos_of = {int(r): p for p, r in enumerate(srv_ids)}
             name_id = {nm: i for i, nm in enumerate(self.planet.names)}
+            for names, _ in (x for lst in configs.values() for x in lst):
+                for x in names:
+                    if x not in name_id or name_id[x] not in pos_of:
+                        raise ValueError(f"{filename}: region {x!r} is not a server of this search's planet")
             per_n = {}
             for n, lst in configs.items():
                 cfg = np.zeros((len(lst), n), np.uint32)
@@ -414,7 +418,9 @@ class Search:
     # ------------------------------------------------------------ ranking ---
     def _rank(self, configs: Dict[int, dict], p: RankingParams, ci: int):
         """search.rs:329-354: valid configs and their scores, per n, in enumeration order.
-        Scores and validity come from the device (bote_eval with the ranking params)."""
+        Scores and validity come from the device (bote_eval with the ranking params);
+        a search loaded from a .data file is ranked from the file's histograms only,
+        as the reference ranks its stored ProtocolStats (compute_score_host)."""
         ranked = {}
         for n, d in configs.items():
             if not (p.min_n <= n <= p.max_n):
@@ -422,6 +428,14 @@ class Search:
             cfg = d["cfg"]
             if len(cfg) == 0:
                 ranked[n] = []
+                continue
+            if (ci, n, 0) in self._file_stats:
+                out = []
+                for i in range(len(cfg)):
+                    ok, score = compute_score_host(n, self._stats(ci, n, i), p)
+                    if ok:
+                        out.append((score.value(), i))
+                ranked[n] = out
                 continue
             r = eval_configs(self.dp, d["srv"], d["cli"], n, configs=cfg, ranking=p, values=False)
             idx = np.nonzero(r.valid)[0]
@@ -482,6 +496,26 @@ class Search:
         return out
 
 
+def compute_score_host(n: int, stats: ProtocolStats, p: RankingParams) -> Tuple[bool, F64]:
+    """search.rs:421-472 on host histograms (for searches loaded from a .data
+    file, whose stats are the file's, not the device's): F64 arithmetic in the
+    reference's order; `>=` is the derived PartialOrd (plain f64)."""
+    valid = True
+    score = F64.zero()
+    inp = ClientPlacement.Input
+    for f in p.ft_metric.fs(n):
+        atlas = stats.get(Protocol.Atlas, f, inp)
+        fpaxos = stats.get(Protocol.FPaxos, f, inp)
+        fmi = fpaxos.mean_improv(atlas)
+        ffi = fpaxos.cov_improv(atlas)
+        valid = valid and fmi.ge(F64(p.min_mean_fpaxos_improv)) and ffi.ge(F64(p.min_fairness_fpaxos_improv))
+        emi = stats.get(Protocol.EPaxos, 0, inp).mean_improv(atlas)
+        if n in (11, 13):
+            valid = valid and emi.ge(F64(p.min_mean_epaxos_improv))
+        score = score + (fmi + F64(30.0) * emi)
+    return valid, score
+
+
 # ---------------------------------------------------------------- sweep ---
 DEFAULT_OBJECTIVES = [(_lib.OBJ_SCORE, 0), (_lib.OBJ_MEAN, _lib.SLOT_AF1), (_lib.OBJ_MEAN, _lib.SLOT_FF1),
                       (_lib.OBJ_COV, _lib.SLOT_AF1), (_lib.OBJ_MEAN, _lib.SLOT_E)]
@@ -500,15 +534,19 @@ class Sweep:
 
     def __init__(self, dp: DevicePlanet, servers: Sequence[int], clients: Sequence[int], n: int,
                  objectives=DEFAULT_OBJECTIVES, K: int = 100, ranking: Optional[RankingParams] = DEFAULT_RANKING,
-                 digest: bool = False):
+                 digest: bool = False, kernel: Optional[str] = None):
+        """kernel: None/'auto' (the library's choice), or force 'generic', 'fast'
+        or 'group' (every path is exact; bote_sweep_create_ex)."""
         self.dp, self.n, self.K = dp, n, K
         self.servers, self.clients = u32(servers), u32(clients)
         self.objectives = list(objectives)
+        self.ranking, self.digest = ranking, bool(digest)
         objs = (_lib.Objective * max(len(self.objectives), 1))(*[_lib.Objective(k, s) for k, s in self.objectives])
         rp = C.byref(_lib.ranking_params_c(ranking)) if ranking is not None else None
         h = C.c_void_p()
-        check(lib().bote_sweep_create(dp.h, self.servers, len(self.servers), self.clients, len(self.clients), n,
-                                      objs, len(self.objectives), K, rp, 1 if digest else 0, C.byref(h)))
+        check(lib().bote_sweep_create_ex(dp.h, self.servers, len(self.servers), self.clients, len(self.clients), n,
+                                         objs, len(self.objectives), K, rp, 1 if digest else 0,
+                                         _lib.KERNELS[kernel], C.byref(h)))
         self.h = h
         self.total = _lib.binomial(len(self.servers), n)
 
@@ -534,8 +572,15 @@ class Sweep:
         re = self.total if rank_end is None else rank_end
         if not 0 <= rank_begin <= re <= self.total or chunk < 1:
             raise ValueError("bad rank range or chunk")
-        ident = np.concatenate([np.array([self.n, self.K, rank_begin, re, len(self.servers), len(self.clients)],
-                                         np.uint64), self.servers.astype(np.uint64), self.clients.astype(np.uint64),
+        rk = self.ranking
+        # ranking params as raw f64 bits, plus the digest flag: a checkpoint
+        # scored under other thresholds (or without the digest) is refused
+        rbits = (np.array([rk.min_mean_fpaxos_improv, rk.min_mean_epaxos_improv, rk.min_fairness_fpaxos_improv,
+                           rk.min_mean_decrease], np.float64).view(np.uint64).tolist() + [rk.ft_metric.value]
+                 if rk is not None else [0xFFFFFFFFFFFFFFFF] * 5)
+        ident = np.concatenate([np.array([self.n, self.K, rank_begin, re, len(self.servers), len(self.clients),
+                                          int(self.digest)] + rbits, np.uint64),
+                                self.servers.astype(np.uint64), self.clients.astype(np.uint64),
                                 np.asarray(self.objectives, np.uint64).reshape(-1),
                                 np.asarray(self.dp.planet.lat, np.uint64).reshape(-1)])
         dev = torch.device("cuda", self.dp.device)
@@ -640,3 +685,25 @@ class Sweep:
     def config_of(self, rank: int) -> List[int]:
         pos = _lib.colex_unrank(rank, self.n, len(self.servers))
         return [int(self.servers[p]) for p in pos]
+
+
+def search_topk(planets: Sequence[DevicePlanet], servers: Sequence[int], clients: Sequence[int], n: int,
+                objectives=DEFAULT_OBJECTIVES, K: int = 100, ranking: Optional[RankingParams] = DEFAULT_RANKING,
+                digest: bool = True, rank_begin: int = 0, rank_end: Optional[int] = None) -> SweepResult:
+    """bote_search_topk: the sweep sharded over `planets` (one per shard; the
+    same device may appear more than once) in ONE library call, merged on
+    planets[0]'s device.  The multi-GPU search without torch.distributed."""
+    srv, cli = u32(servers), u32(clients)
+    objs_l = list(objectives)
+    no = len(objs_l)
+    objs = (_lib.Objective * max(no, 1))(*[_lib.Objective(k, s) for k, s in objs_l])
+    rp = C.byref(_lib.ranking_params_c(ranking)) if ranking is not None else None
+    hs = (C.c_void_p * len(planets))(*[p.h.value for p in planets])
+    re = _lib.binomial(len(srv), n) if rank_end is None else rank_end
+    recs = (_lib.TopKRecord * max(no * K, 1))()
+    cnt = np.zeros(max(no, 1), np.uint32)
+    valid, dig = C.c_uint64(), C.c_uint64()
+    check(lib().bote_search_topk(hs, len(planets), srv, len(srv), cli, len(cli), n, rank_begin, re, objs, no, K, rp,
+                                 1 if digest else 0, recs, ptr(cnt), C.byref(valid), C.byref(dig)))
+    tops = [[(recs[o * K + i].key, recs[o * K + i].rank) for i in range(cnt[o])] for o in range(no)]
+    return SweepResult(tops, valid.value, dig.value)

@@ -8,6 +8,7 @@
 
 #include <algorithm>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -33,13 +34,27 @@ int fail(int code, const std::string& msg) {
     if (_e != hipSuccess) return fail(BOTE_E_DEVICE, std::string(#expr) + ": " + hipGetErrorString(_e)); \
   } while (0)
 
-// RAII device buffer
+// RAII device buffer; reserve() grows it (grow-only, for cached workspaces)
 struct DBuf {
   void* p = nullptr;
+  size_t cap = 0;
+  DBuf() = default;
+  DBuf(const DBuf&) = delete;
+  DBuf& operator=(const DBuf&) = delete;
   ~DBuf() {
     if (p) (void)hipFree(p);
   }
-  hipError_t alloc(size_t bytes) { return hipMalloc(&p, bytes ? bytes : 16); }
+  hipError_t alloc(size_t bytes) {
+    cap = bytes ? bytes : 16;
+    return hipMalloc(&p, cap);
+  }
+  hipError_t reserve(size_t bytes) {
+    if (bytes <= cap && p) return hipSuccess;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    return alloc(std::max(bytes, 2 * cap));
+  }
   template <class T>
   T* as() const { return (T*)p; }
 };
@@ -95,11 +110,19 @@ size_t device_max_lds(int dev) {
 
 }  // namespace
 
+// A planet resident on one device.  The per-call entry points (bote_eval,
+// bote_leaderless, ...) run stream-ordered on the planet's own non-blocking
+// stream with cached, grow-only device workspaces; calls on one handle are
+// serialised by its mutex, calls on distinct handles are independent (no
+// device-wide synchronisation anywhere).
 struct bote_planet {
   int device;
   uint32_t R;
   std::vector<uint16_t> lat;
   uint32_t* d_mat = nullptr;
+  hipStream_t stream = nullptr;
+  mutable std::mutex mu;
+  mutable DBuf ws[12];
 };
 
 struct bote_sweep {
@@ -109,6 +132,9 @@ struct bote_sweep {
   uint32_t grid = 0, bd = 0;
   size_t shm = 0;
   DBuf srv, cli, binom, top, tmp0, tmp1, result, counters;
+  // overflow fallback of the fast path (generic kernel over the whole range,
+  // run only when the deferred queue overflowed; chosen on the device)
+  DBuf top_alt, counters_alt;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   // per-launch kernel timing since the last bote_sweep_timing_reset
   std::vector<std::pair<hipEvent_t, hipEvent_t>> evpool;
@@ -216,10 +242,11 @@ int bote_planet_create(const uint16_t* lat, uint32_t R, int device, bote_planet*
     delete p;
     return fail(BOTE_E_NOMEM, "hipMalloc planet");
   }
-  if (hipMemcpy(p->d_mat, m.data(), m.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
+  if (hipMemcpy(p->d_mat, m.data(), m.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
+      hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking) != hipSuccess) {
     (void)hipFree(p->d_mat);
     delete p;
-    return fail(BOTE_E_DEVICE, "upload planet");
+    return fail(BOTE_E_DEVICE, "upload planet / create its stream");
   }
   *out = p;
   return BOTE_OK;
@@ -228,7 +255,9 @@ int bote_planet_create(const uint16_t* lat, uint32_t R, int device, bote_planet*
 int bote_planet_destroy(bote_planet* p) {
   if (!p) return BOTE_OK;
   (void)hipSetDevice(p->device);
+  if (p->stream) (void)hipStreamSynchronize(p->stream);
   if (p->d_mat) (void)hipFree(p->d_mat);
+  if (p->stream) (void)hipStreamDestroy(p->stream);
   delete p;
   return BOTE_OK;
 }
@@ -283,15 +312,17 @@ static int run_single(const bote_planet* p, const uint32_t* servers, uint32_t ns
   if (mode == 2 && leader >= p->R) return fail(BOTE_E_ARG, "leader out of range");
   if (q == 0) return fail(BOTE_E_ARG, "quorum size 0");
   if (q > distinct_count(servers, ns, p->R)) return fail(BOTE_E_QUORUM_GT_N, "quorum larger than the server set");
+  std::lock_guard<std::mutex> lk(p->mu);
   HIP_TRY(hipSetDevice(p->device));
-  DBuf ds, dc, df, dout;
-  HIP_TRY(ds.alloc(ns * 4));
-  HIP_TRY(dc.alloc(nc * 4));
-  HIP_TRY(df.alloc(nf * 4));
-  HIP_TRY(dout.alloc(nout * 8));
-  if (ns) HIP_TRY(hipMemcpy(ds.p, servers, ns * 4, hipMemcpyHostToDevice));
-  if (nc) HIP_TRY(hipMemcpy(dc.p, clients, nc * 4, hipMemcpyHostToDevice));
-  if (nf) HIP_TRY(hipMemcpy(df.p, froms, nf * 4, hipMemcpyHostToDevice));
+  hipStream_t st = p->stream;
+  DBuf &ds = p->ws[0], &dc = p->ws[1], &df = p->ws[2], &dout = p->ws[3];
+  HIP_TRY(ds.reserve(ns * 4));
+  HIP_TRY(dc.reserve(nc * 4));
+  HIP_TRY(df.reserve(nf * 4));
+  HIP_TRY(dout.reserve(nout * 8));
+  if (ns) HIP_TRY(hipMemcpyAsync(ds.p, servers, ns * 4, hipMemcpyHostToDevice, st));
+  if (nc) HIP_TRY(hipMemcpyAsync(dc.p, clients, nc * 4, hipMemcpyHostToDevice, st));
+  if (nf) HIP_TRY(hipMemcpyAsync(df.p, froms, nf * 4, hipMemcpyHostToDevice, st));
   SingleArgs a{};
   a.mat = p->d_mat;
   a.R = p->R;
@@ -304,9 +335,9 @@ static int run_single(const bote_planet* p, const uint32_t* servers, uint32_t ns
   a.q = q;
   a.leader = leader;
   a.out = dout.as<uint64_t>();
-  HIP_TRY(bote::launch_single(a, mode, nullptr));
-  HIP_TRY(hipDeviceSynchronize());
-  if (nout) HIP_TRY(hipMemcpy(out, dout.p, nout * 8, hipMemcpyDeviceToHost));
+  HIP_TRY(bote::launch_single(a, mode, st));
+  if (nout) HIP_TRY(hipMemcpyAsync(out, dout.p, nout * 8, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
   return BOTE_OK;
 }
 
@@ -340,15 +371,17 @@ int bote_best_leader(const bote_planet* p, const uint32_t* servers, uint32_t ns,
   if ((rc = check_regions(clients, nc, p->R, false, "clients"))) return rc;
   if (q == 0) return fail(BOTE_E_ARG, "quorum size 0");
   if (q > distinct_count(servers, ns, p->R)) return fail(BOTE_E_QUORUM_GT_N, "quorum larger than the server set");
+  std::lock_guard<std::mutex> lk(p->mu);
   HIP_TRY(hipSetDevice(p->device));
-  DBuf ds, dc, dv, dstat, dpos;
-  HIP_TRY(ds.alloc(ns * 4));
-  HIP_TRY(dc.alloc(nc * 4));
-  HIP_TRY(dv.alloc((size_t)ns * nc * 8));
-  HIP_TRY(dstat.alloc(ns * 8));
-  HIP_TRY(dpos.alloc(4));
-  HIP_TRY(hipMemcpy(ds.p, servers, ns * 4, hipMemcpyHostToDevice));
-  if (nc) HIP_TRY(hipMemcpy(dc.p, clients, nc * 4, hipMemcpyHostToDevice));
+  hipStream_t st = p->stream;
+  DBuf &ds = p->ws[0], &dc = p->ws[1], &dv = p->ws[2], &dstat = p->ws[3], &dpos = p->ws[4];
+  HIP_TRY(ds.reserve(ns * 4));
+  HIP_TRY(dc.reserve(nc * 4));
+  HIP_TRY(dv.reserve((size_t)ns * nc * 8));
+  HIP_TRY(dstat.reserve(ns * 8));
+  HIP_TRY(dpos.reserve(4));
+  HIP_TRY(hipMemcpyAsync(ds.p, servers, ns * 4, hipMemcpyHostToDevice, st));
+  if (nc) HIP_TRY(hipMemcpyAsync(dc.p, clients, nc * 4, hipMemcpyHostToDevice, st));
   SingleArgs a{};
   a.mat = p->d_mat;
   a.R = p->R;
@@ -360,12 +393,14 @@ int bote_best_leader(const bote_planet* p, const uint32_t* servers, uint32_t ns,
   a.stat = stat;
   a.out = dv.as<uint64_t>();
   a.out_pos = dpos.as<uint32_t>();
-  HIP_TRY(bote::launch_single(a, 3, nullptr));
-  HIP_TRY(bote::launch_best_leader(a, dv.as<uint64_t>(), dstat.as<double>(), nullptr));
-  HIP_TRY(hipDeviceSynchronize());
-  HIP_TRY(hipMemcpy(out_pos, dpos.p, 4, hipMemcpyDeviceToHost));
-  if (out_lat && nc)
-    HIP_TRY(hipMemcpy(out_lat, dv.as<uint64_t>() + (size_t)(*out_pos) * nc, nc * 8, hipMemcpyDeviceToHost));
+  HIP_TRY(bote::launch_single(a, 3, st));
+  HIP_TRY(bote::launch_best_leader(a, dv.as<uint64_t>(), dstat.as<double>(), st));
+  HIP_TRY(hipMemcpyAsync(out_pos, dpos.p, 4, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  if (out_lat && nc) {
+    HIP_TRY(hipMemcpyAsync(out_lat, dv.as<uint64_t>() + (size_t)(*out_pos) * nc, nc * 8, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+  }
   return BOTE_OK;
 }
 
@@ -416,13 +451,17 @@ int bote_eval(const bote_planet* p, const uint32_t* servers, uint32_t ns, const 
     uint64_t total = binom_u64(ns, n);
     if (rank_begin > total || ncfg > total - rank_begin) return fail(BOTE_E_ARG, "rank range out of bounds");
   }
+  std::lock_guard<std::mutex> lk(p->mu);
   HIP_TRY(hipSetDevice(p->device));
+  hipStream_t st = p->stream;
   const size_t stride = 5ull * nc + 5ull * n;
-  DBuf ds, dc, dcfg, dbin, dvals, dlead, ds1, ds2, dmean, dcov, dscore, dvalid;
-  HIP_TRY(ds.alloc(ns * 4));
-  HIP_TRY(dc.alloc(nc * 4));
-  HIP_TRY(hipMemcpy(ds.p, servers, ns * 4, hipMemcpyHostToDevice));
-  if (nc) HIP_TRY(hipMemcpy(dc.p, clients, nc * 4, hipMemcpyHostToDevice));
+  DBuf &ds = p->ws[0], &dc = p->ws[1], &dcfg = p->ws[2], &dbin = p->ws[3], &dvals = p->ws[4], &dlead = p->ws[5],
+       &ds1 = p->ws[6], &ds2 = p->ws[7], &dmean = p->ws[8], &dcov = p->ws[9], &dscore = p->ws[10],
+       &dvalid = p->ws[11];
+  HIP_TRY(ds.reserve(ns * 4));
+  HIP_TRY(dc.reserve(nc * 4));
+  HIP_TRY(hipMemcpyAsync(ds.p, servers, ns * 4, hipMemcpyHostToDevice, st));
+  if (nc) HIP_TRY(hipMemcpyAsync(dc.p, clients, nc * 4, hipMemcpyHostToDevice, st));
   EvalArgs a{};
   a.mat = p->d_mat;
   a.R = p->R;
@@ -431,30 +470,31 @@ int bote_eval(const bote_planet* p, const uint32_t* servers, uint32_t ns, const 
   a.cli = dc.as<uint32_t>();
   a.nc = nc;
   a.srv_sorted = std::is_sorted(servers, servers + ns) ? 1 : 0;
+  std::vector<uint64_t> t;
   if (configs) {
-    HIP_TRY(dcfg.alloc(ncfg * n * 4));
-    HIP_TRY(hipMemcpy(dcfg.p, configs, ncfg * n * 4, hipMemcpyHostToDevice));
+    HIP_TRY(dcfg.reserve(ncfg * n * 4));
+    HIP_TRY(hipMemcpyAsync(dcfg.p, configs, ncfg * n * 4, hipMemcpyHostToDevice, st));
     a.cfgs = dcfg.as<uint32_t>();
     a.rb = 0;
     a.re = ncfg;
   } else {
-    auto t = binom_table(ns, n);
-    HIP_TRY(dbin.alloc(t.size() * 8));
-    HIP_TRY(hipMemcpy(dbin.p, t.data(), t.size() * 8, hipMemcpyHostToDevice));
+    t = binom_table(ns, n);
+    HIP_TRY(dbin.reserve(t.size() * 8));
+    HIP_TRY(hipMemcpyAsync(dbin.p, t.data(), t.size() * 8, hipMemcpyHostToDevice, st));
     a.binom = dbin.as<uint64_t>();
     a.rb = rank_begin;
     a.re = rank_begin + ncfg;
   }
   a.runlen = 1;
   fill_rank_params(a, rp);
-  if (out_vals) { HIP_TRY(dvals.alloc(ncfg * stride * 4)); a.out_vals = dvals.as<uint32_t>(); }
-  if (out_leader) { HIP_TRY(dlead.alloc(ncfg * 4)); a.out_leader = dlead.as<uint32_t>(); }
-  if (out_sum) { HIP_TRY(ds1.alloc(ncfg * bote::NSLOT * 8)); a.out_s1 = ds1.as<uint64_t>(); }
-  if (out_sumsq) { HIP_TRY(ds2.alloc(ncfg * bote::NSLOT * 8)); a.out_s2 = ds2.as<uint64_t>(); }
-  if (out_mean) { HIP_TRY(dmean.alloc(ncfg * bote::NSLOT * 8)); a.out_mean = dmean.as<double>(); }
-  if (out_cov) { HIP_TRY(dcov.alloc(ncfg * bote::NSLOT * 8)); a.out_cov = dcov.as<double>(); }
-  if (out_score && rp) { HIP_TRY(dscore.alloc(ncfg * 8)); a.out_score = dscore.as<double>(); }
-  if (out_valid && rp) { HIP_TRY(dvalid.alloc(ncfg)); a.out_valid = dvalid.as<uint8_t>(); }
+  if (out_vals) { HIP_TRY(dvals.reserve(ncfg * stride * 4)); a.out_vals = dvals.as<uint32_t>(); }
+  if (out_leader) { HIP_TRY(dlead.reserve(ncfg * 4)); a.out_leader = dlead.as<uint32_t>(); }
+  if (out_sum) { HIP_TRY(ds1.reserve(ncfg * bote::NSLOT * 8)); a.out_s1 = ds1.as<uint64_t>(); }
+  if (out_sumsq) { HIP_TRY(ds2.reserve(ncfg * bote::NSLOT * 8)); a.out_s2 = ds2.as<uint64_t>(); }
+  if (out_mean) { HIP_TRY(dmean.reserve(ncfg * bote::NSLOT * 8)); a.out_mean = dmean.as<double>(); }
+  if (out_cov) { HIP_TRY(dcov.reserve(ncfg * bote::NSLOT * 8)); a.out_cov = dcov.as<double>(); }
+  if (out_score && rp) { HIP_TRY(dscore.reserve(ncfg * 8)); a.out_score = dscore.as<double>(); }
+  if (out_valid && rp) { HIP_TRY(dvalid.reserve(ncfg)); a.out_valid = dvalid.as<uint8_t>(); }
 
   const uint32_t bd = 256;
   size_t shm = bote::eval_smem_bytes(a, n, bd, false);
@@ -462,16 +502,17 @@ int bote_eval(const bote_planet* p, const uint32_t* servers, uint32_t ns, const 
   int nb = bote::eval_occupancy(n, true, bd, shm);
   uint64_t want = (ncfg + bd - 1) / bd;
   uint32_t grid = (uint32_t)std::min<uint64_t>(want, (uint64_t)device_cus(p->device) * nb);
-  HIP_TRY(bote::launch_eval(a, n, true, grid, bd, shm, nullptr));
-  HIP_TRY(hipDeviceSynchronize());
-  if (out_vals) HIP_TRY(hipMemcpy(out_vals, dvals.p, ncfg * stride * 4, hipMemcpyDeviceToHost));
-  if (out_leader) HIP_TRY(hipMemcpy(out_leader, dlead.p, ncfg * 4, hipMemcpyDeviceToHost));
-  if (out_sum) HIP_TRY(hipMemcpy(out_sum, ds1.p, ncfg * bote::NSLOT * 8, hipMemcpyDeviceToHost));
-  if (out_sumsq) HIP_TRY(hipMemcpy(out_sumsq, ds2.p, ncfg * bote::NSLOT * 8, hipMemcpyDeviceToHost));
-  if (out_mean) HIP_TRY(hipMemcpy(out_mean, dmean.p, ncfg * bote::NSLOT * 8, hipMemcpyDeviceToHost));
-  if (out_cov) HIP_TRY(hipMemcpy(out_cov, dcov.p, ncfg * bote::NSLOT * 8, hipMemcpyDeviceToHost));
-  if (out_score && rp) HIP_TRY(hipMemcpy(out_score, dscore.p, ncfg * 8, hipMemcpyDeviceToHost));
-  if (out_valid && rp) HIP_TRY(hipMemcpy(out_valid, dvalid.p, ncfg, hipMemcpyDeviceToHost));
+  HIP_TRY(bote::launch_eval(a, n, true, grid, bd, shm, st));
+  const hipMemcpyKind D2H = hipMemcpyDeviceToHost;
+  if (out_vals) HIP_TRY(hipMemcpyAsync(out_vals, dvals.p, ncfg * stride * 4, D2H, st));
+  if (out_leader) HIP_TRY(hipMemcpyAsync(out_leader, dlead.p, ncfg * 4, D2H, st));
+  if (out_sum) HIP_TRY(hipMemcpyAsync(out_sum, ds1.p, ncfg * bote::NSLOT * 8, D2H, st));
+  if (out_sumsq) HIP_TRY(hipMemcpyAsync(out_sumsq, ds2.p, ncfg * bote::NSLOT * 8, D2H, st));
+  if (out_mean) HIP_TRY(hipMemcpyAsync(out_mean, dmean.p, ncfg * bote::NSLOT * 8, D2H, st));
+  if (out_cov) HIP_TRY(hipMemcpyAsync(out_cov, dcov.p, ncfg * bote::NSLOT * 8, D2H, st));
+  if (out_score && rp) HIP_TRY(hipMemcpyAsync(out_score, dscore.p, ncfg * 8, D2H, st));
+  if (out_valid && rp) HIP_TRY(hipMemcpyAsync(out_valid, dvalid.p, ncfg, D2H, st));
+  HIP_TRY(hipStreamSynchronize(st));
   return BOTE_OK;
 }
 
@@ -479,8 +520,15 @@ int bote_eval(const bote_planet* p, const uint32_t* servers, uint32_t ns, const 
 int bote_sweep_create(const bote_planet* p, const uint32_t* servers, uint32_t ns, const uint32_t* clients,
                       uint32_t nc, uint32_t n, const bote_objective* objs, uint32_t n_obj, uint32_t K,
                       const bote_ranking_params* rp, int digest, bote_sweep** out) {
+  return bote_sweep_create_ex(p, servers, ns, clients, nc, n, objs, n_obj, K, rp, digest, BOTE_KERNEL_AUTO, out);
+}
+
+int bote_sweep_create_ex(const bote_planet* p, const uint32_t* servers, uint32_t ns, const uint32_t* clients,
+                         uint32_t nc, uint32_t n, const bote_objective* objs, uint32_t n_obj, uint32_t K,
+                         const bote_ranking_params* rp, int digest, int kernel, bote_sweep** out) {
   int rc;
   if (!out) return fail(BOTE_E_ARG, "out is null");
+  if (kernel < BOTE_KERNEL_AUTO || kernel > BOTE_KERNEL_GROUP) return fail(BOTE_E_ARG, "unknown kernel path");
   if ((rc = check_search_args(p, servers, ns, clients, nc, n))) return rc;
   if (n_obj > BOTE_MAX_OBJECTIVES) return fail(BOTE_E_RANGE, "more than 8 objectives");
   if (n_obj && !objs) return fail(BOTE_E_ARG, "objectives null");
@@ -548,12 +596,12 @@ int bote_sweep_create(const bote_planet* p, const uint32_t* servers, uint32_t ns
   s->grid = (uint32_t)(device_cus(p->device) * nb);
   s->xgrid = 32;
 
-  // ---- fast path: quad layouts, column sums are computed on the device
-  // BOTE_SWEEP_KERNEL=generic|fast|group forces a path (tests, A/B timing);
-  // by default: group kernel when eligible and >= 90 % lane utilisation.
-  const char* kern = getenv("BOTE_SWEEP_KERNEL");
-  const bool force_generic = getenv("BOTE_FORCE_GENERIC") || (kern && !strcmp(kern, "generic"));
-  s->fast = fast_eligible(p, servers, ns, nc, has_score ? rp : nullptr) && !force_generic;
+  // ---- fast path: quad layouts, column sums are computed on the device.
+  // `kernel` forces a path (tests, A/B timing; every path is exact); AUTO:
+  // the group kernel when eligible and >= 90 % lane utilisation.
+  s->fast = fast_eligible(p, servers, ns, nc, has_score ? rp : nullptr) && kernel != BOTE_KERNEL_GENERIC;
+  if (kernel != BOTE_KERNEL_AUTO && kernel != BOTE_KERNEL_GENERIC && !s->fast)
+    return cleanup(fail(BOTE_E_ARG, "the fast/group kernel is not eligible for this planet and lists"));
   if (s->fast) {
     bote::FastArgs& f = s->fargs;
     f = bote::FastArgs{};
@@ -605,8 +653,10 @@ int bote_sweep_create(const bote_planet* p, const uint32_t* servers, uint32_t ns
     f.queue = s->queue.as<uint64_t>();
     f.queue_count = s->qcount.as<unsigned long long>();
     f.queue_cap = QUEUE_CAP;
-    const char* abl = getenv("BOTE_ABLATE");  // timing diagnostics only
+#ifdef BOTE_ABLATION
+    const char* abl = getenv("BOTE_ABLATE");  // timing-diagnostics builds only
     f.ablate = abl ? (uint32_t)strtoul(abl, nullptr, 0) : 0u;
+#endif
     s->fshm = bote::fast_smem_bytes(f, n);
     if (s->fshm > device_max_lds(p->device)) {
       s->fast = false;
@@ -615,7 +665,8 @@ int bote_sweep_create(const bote_planet* p, const uint32_t* servers, uint32_t ns
     }
     // group kernel: n >= 4, positions fit 8 bits, enough lane utilisation
     bool want_group = n >= 4 && ns <= 256 && group_utilisation(ns, n) >= 0.9;
-    if (kern) want_group = n >= 4 && ns <= 256 && !strcmp(kern, "group");
+    if (kernel != BOTE_KERNEL_AUTO) want_group = n >= 4 && ns <= 256 && kernel == BOTE_KERNEL_GROUP;
+    if (kernel == BOTE_KERNEL_GROUP && !want_group) return cleanup(fail(BOTE_E_ARG, "group kernel needs n >= 4"));
     if (s->fast && want_group) {
       auto lt = low_table(ns - (n - 3));
       if (s->lowtab.alloc(std::max<size_t>(lt.size(), 1) * 4) != hipSuccess)
@@ -627,7 +678,7 @@ int bote_sweep_create(const bote_planet* p, const uint32_t* servers, uint32_t ns
       // bote.py DEFAULT_OBJECTIVES: SCORE, MEAN af1, MEAN ff1, COV af1, MEAN e
       static const uint32_t dk[5] = {BOTE_OBJ_SCORE, BOTE_OBJ_MEAN, BOTE_OBJ_MEAN, BOTE_OBJ_COV, BOTE_OBJ_MEAN};
       static const uint32_t ds[5] = {0, BOTE_SLOT_AF1, BOTE_SLOT_FF1, BOTE_SLOT_AF1, BOTE_SLOT_E};
-      s->def_obj = n_obj == 5 && f.want_score && !getenv("BOTE_NO_DEF_OBJ");
+      s->def_obj = n_obj == 5 && f.want_score;
       for (uint32_t o = 0; s->def_obj && o < 5; ++o)
         s->def_obj = objs[o].kind == dk[o] && (dk[o] == BOTE_OBJ_SCORE || objs[o].slot == ds[o]);
       if (gshm <= device_max_lds(p->device)) {
@@ -644,6 +695,9 @@ int bote_sweep_create(const bote_planet* p, const uint32_t* servers, uint32_t ns
   if (s->top.alloc(top_bytes) != hipSuccess || s->tmp0.alloc(tmp_bytes) != hipSuccess ||
       s->tmp1.alloc(tmp_bytes) != hipSuccess || s->result.alloc(s->result_bytes()) != hipSuccess)
     return cleanup(fail(BOTE_E_NOMEM, "hipMalloc sweep workspace"));
+  if (s->fast && (s->top_alt.alloc((size_t)s->grid * std::max<uint32_t>(n_obj, 1) * bote::KP * 16) != hipSuccess ||
+                  s->counters_alt.alloc(16) != hipSuccess))
+    return cleanup(fail(BOTE_E_NOMEM, "hipMalloc overflow fallback workspace"));
   a.out_top = n_obj ? s->top.as<Rec>() : nullptr;
   s->fargs.out_top = a.out_top;
   if (hipEventCreate(&s->ev0) != hipSuccess || hipEventCreate(&s->ev1) != hipSuccess)
@@ -659,22 +713,40 @@ int bote_sweep_is_fast(const bote_sweep* s, int* out) {
 }
 
 // Merge `lists` per-block lists into the result block and append the counters.
-static int merge_chain(bote_sweep* s, uint32_t lists, hipStream_t st) {
+// With `sel` (fast path), the first level reads the overflow fallback's
+// `alt_lists` lists and counters instead when *sel > QUEUE_CAP (on the device).
+static int merge_chain(bote_sweep* s, uint32_t lists, hipStream_t st, const unsigned long long* sel = nullptr,
+                       uint32_t alt_lists = 0) {
   const uint64_t lstride = (uint64_t)s->n_obj * bote::KP;
   Rec* rec_out = s->result.as<Rec>();
   if (s->n_obj) {
     const Rec* src = s->top.as<Rec>();
     Rec* bufs[2] = {s->tmp0.as<Rec>(), s->tmp1.as<Rec>()};
     int b = 0;
+    if (sel) {
+      Rec* dst = lists > bote::G_MERGE_LISTS || alt_lists > bote::G_MERGE_LISTS ? bufs[b] : rec_out;
+      HIP_TRY(bote::launch_merge_sel(src, lists, s->top_alt.as<Rec>(), alt_lists, lstride, sel, QUEUE_CAP, dst, lstride,
+                                     s->n_obj, st));
+      lists = (std::max(lists, alt_lists) + bote::G_MERGE_LISTS - 1) / bote::G_MERGE_LISTS;
+      src = dst;
+      b ^= 1;
+      if (dst == rec_out) lists = 0;
+    }
     while (lists > bote::G_MERGE_LISTS) {
       HIP_TRY(bote::launch_merge(src, lists, lstride, bufs[b], lstride, s->n_obj, st));
       src = bufs[b];
       b ^= 1;
       lists = (lists + bote::G_MERGE_LISTS - 1) / bote::G_MERGE_LISTS;
     }
-    HIP_TRY(bote::launch_merge(src, lists, lstride, rec_out, lstride, s->n_obj, st));
+    if (lists) HIP_TRY(bote::launch_merge(src, lists, lstride, rec_out, lstride, s->n_obj, st));
   }
-  HIP_TRY(hipMemcpyAsync((char*)s->result.p + lstride * 16, s->counters.p, 16, hipMemcpyDeviceToDevice, st));
+  uint64_t* cdst = (uint64_t*)((char*)s->result.p + lstride * 16);
+  if (sel) {
+    HIP_TRY(bote::launch_pick_counters(s->counters.as<unsigned long long>(), s->counters_alt.as<unsigned long long>(),
+                                       sel, QUEUE_CAP, cdst, st));
+  } else {
+    HIP_TRY(hipMemcpyAsync(cdst, s->counters.p, 16, hipMemcpyDeviceToDevice, st));
+  }
   return BOTE_OK;
 }
 
@@ -739,22 +811,22 @@ static int launch_fast_path(bote_sweep* s, uint64_t rb, uint64_t re, hipStream_t
   a.runlen = 1;
   a.out_top = s->n_obj ? s->top.as<Rec>() + (size_t)s->fgrid * s->n_obj * bote::KP : nullptr;
   HIP_TRY(bote::launch_eval(a, s->n, false, s->xgrid, s->bd, s->shm, st));
-  return merge_chain(s, s->fgrid + s->xgrid, st);
-}
-
-// After a fast-path launch: if more configs were deferred than the queue
-// holds, recompute the whole range on the generic path (synchronous).
-static int ensure_complete(bote_sweep* s, hipStream_t st) {
-  if (!s->fast) return BOTE_OK;
-  unsigned long long q = 0;
-  HIP_TRY(hipMemcpyAsync(&q, s->qcount.p, 8, hipMemcpyDeviceToHost, st));
-  HIP_TRY(hipStreamSynchronize(st));
-  if (q <= QUEUE_CAP) return BOTE_OK;
-  int rc = launch_generic(s, s->last_rb, s->last_re, st, false);
-  if (rc) return rc;
-  HIP_TRY(hipMemsetAsync(s->qcount.p, 0, 8, st));
-  HIP_TRY(hipStreamSynchronize(st));
-  return BOTE_OK;
+  // overflow fallback: more deferred configs than the queue holds => the
+  // generic kernel recomputes the whole range into its own lists/counters and
+  // the merge picks those.  Decided on the device (every block of the fallback
+  // exits at once otherwise): no host round trip per launch.
+  EvalArgs g = s->args;
+  g.rb = rb;
+  g.re = re;
+  const uint64_t GG = (uint64_t)s->grid * s->bd;
+  g.runlen = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(32, count / (GG * 8)));
+  g.out_top = s->n_obj ? s->top_alt.as<Rec>() : nullptr;
+  g.out_counters = s->counters_alt.as<unsigned long long>();
+  g.run_if_over = s->qcount.as<unsigned long long>();
+  g.over_cap = QUEUE_CAP;
+  HIP_TRY(hipMemsetAsync(s->counters_alt.p, 0, 16, st));
+  HIP_TRY(bote::launch_eval(g, s->n, false, s->grid, s->bd, s->shm, st));
+  return merge_chain(s, s->fgrid + s->xgrid, st, s->qcount.as<unsigned long long>(), s->grid);
 }
 
 int bote_sweep_launch(bote_sweep* s, uint64_t rank_begin, uint64_t rank_end, void* hip_stream) {
@@ -778,8 +850,6 @@ int bote_sweep_result_device(bote_sweep* s, void* dst, void* hip_stream) {
   if (!s || !dst) return fail(BOTE_E_ARG, "null argument");
   if (!s->launched) return fail(BOTE_E_ARG, "sweep not launched");
   HIP_TRY(hipSetDevice(s->p->device));
-  int rc = ensure_complete(s, (hipStream_t)hip_stream);
-  if (rc) return rc;
   HIP_TRY(hipMemcpyAsync(dst, s->result.p, s->result_bytes(), hipMemcpyDeviceToDevice, (hipStream_t)hip_stream));
   return BOTE_OK;
 }
@@ -808,8 +878,6 @@ int bote_sweep_result(bote_sweep* s, void* hip_stream, bote_topk_record* out, ui
   if (!s) return fail(BOTE_E_ARG, "sweep is null");
   if (!s->launched) return fail(BOTE_E_ARG, "sweep not launched");
   HIP_TRY(hipSetDevice(s->p->device));
-  int rc = ensure_complete(s, (hipStream_t)hip_stream);
-  if (rc) return rc;
   std::vector<uint8_t> blk(s->result_bytes());
   HIP_TRY(hipMemcpyAsync(blk.data(), s->result.p, blk.size(), hipMemcpyDeviceToHost, (hipStream_t)hip_stream));
   HIP_TRY(hipStreamSynchronize((hipStream_t)hip_stream));
@@ -878,6 +946,126 @@ int bote_sweep_destroy(bote_sweep* s) {
   if (s->ev1) (void)hipEventDestroy(s->ev1);
   delete s;
   return BOTE_OK;
+}
+
+
+// ------------------------------------------------- multi-device search ----
+// SURVEY.md §8b bote_search_topk: the whole sharded search in one call, no
+// PyTorch.  Shard i of [rank_begin, rank_end) sweeps on planets[i]'s device on
+// a stream of its own; the per-shard result blocks meet on planets[0]'s device
+// (peer copies), where a deterministic (key, rank) merge tree combines them.
+// The result equals one unsharded sweep (the merge order does not depend on
+// the number of shards).  Reference: the only parallelism of the reference
+// search is rayon over client sets (search.rs:209-231); this is its
+// replacement for one client set over the GPUs of a node.
+int bote_search_topk(const bote_planet* const* planets, uint32_t n_devices, const uint32_t* servers, uint32_t ns,
+                     const uint32_t* clients, uint32_t nc, uint32_t n, uint64_t rank_begin, uint64_t rank_end,
+                     const bote_objective* objs, uint32_t n_obj, uint32_t K, const bote_ranking_params* rp,
+                     int digest, bote_topk_record* out, uint32_t* out_count, uint64_t* out_valid,
+                     uint64_t* out_digest) {
+  if (!planets || n_devices == 0) return fail(BOTE_E_ARG, "no planets");
+  if (n_devices > 1024) return fail(BOTE_E_RANGE, "at most 1024 shards");
+  for (uint32_t i = 0; i < n_devices; ++i) {
+    if (!planets[i]) return fail(BOTE_E_ARG, "planet is null");
+    if (planets[i]->R != planets[0]->R || planets[i]->lat != planets[0]->lat)
+      return fail(BOTE_E_ARG, "the shards' planets differ");
+  }
+  const uint64_t total = binom_u64(ns, n);
+  if (rank_begin > rank_end || rank_end > total) return fail(BOTE_E_ARG, "rank range out of bounds");
+  struct Shard {
+    bote_sweep* sw = nullptr;
+    hipStream_t st = nullptr;
+    hipEvent_t done = nullptr;
+    DBuf local;
+  };
+  std::vector<Shard> sh(n_devices);
+  const int root = planets[0]->device;
+  hipStream_t rst = nullptr;
+  DBuf gathered, bufa, bufb, merged;
+  int rc = BOTE_OK;
+  auto cleanup = [&](int code) {
+    for (auto& x : sh) {
+      if (x.st) {
+        (void)hipSetDevice(x.sw ? x.sw->p->device : root);
+        (void)hipStreamSynchronize(x.st);
+      }
+    }
+    if (rst) {
+      (void)hipSetDevice(root);
+      (void)hipStreamSynchronize(rst);
+      (void)hipStreamDestroy(rst);
+    }
+    for (auto& x : sh) {
+      const int dev = x.sw ? x.sw->p->device : root;
+      (void)hipSetDevice(dev);
+      if (x.done) (void)hipEventDestroy(x.done);
+      if (x.st) (void)hipStreamDestroy(x.st);
+      if (x.sw) bote_sweep_destroy(x.sw);
+    }
+    return code;
+  };
+  // shards: create, launch (asynchronous, one stream each)
+  for (uint32_t i = 0; i < n_devices; ++i) {
+    if ((rc = bote_sweep_create(planets[i], servers, ns, clients, nc, n, objs, n_obj, K, rp, digest, &sh[i].sw)))
+      return cleanup(rc);
+    HIP_TRY(hipSetDevice(planets[i]->device));
+    if (hipStreamCreateWithFlags(&sh[i].st, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&sh[i].done, hipEventDisableTiming) != hipSuccess)
+      return cleanup(fail(BOTE_E_DEVICE, "shard stream/event"));
+  }
+  const uint64_t span = rank_end - rank_begin;
+  for (uint32_t i = 0; i < n_devices; ++i) {
+    const uint64_t b = rank_begin + (uint64_t)(((unsigned __int128)span * i) / n_devices);
+    const uint64_t e = rank_begin + (uint64_t)(((unsigned __int128)span * (i + 1)) / n_devices);
+    if ((rc = bote_sweep_launch(sh[i].sw, b, e, sh[i].st))) return cleanup(rc);
+  }
+  // gather on the root device
+  const uint64_t nb = sh[0].sw->result_bytes();
+  if (hipSetDevice(root) != hipSuccess || hipStreamCreateWithFlags(&rst, hipStreamNonBlocking) != hipSuccess ||
+      gathered.alloc(nb * n_devices) != hipSuccess || bufa.alloc(nb * ((n_devices + 7) / 8)) != hipSuccess ||
+      bufb.alloc(nb * ((n_devices + 7) / 8)) != hipSuccess || merged.alloc(nb) != hipSuccess)
+    return cleanup(fail(BOTE_E_NOMEM, "gather buffers"));
+  for (uint32_t i = 0; i < n_devices; ++i) {
+    const int dev = planets[i]->device;
+    char* dst = gathered.as<char>() + nb * i;
+    if (dev == root) {
+      if ((rc = bote_sweep_result_device(sh[i].sw, dst, sh[i].st))) return cleanup(rc);
+    } else {
+      HIP_TRY(hipSetDevice(dev));
+      if (sh[i].local.alloc(nb) != hipSuccess) return cleanup(fail(BOTE_E_NOMEM, "shard result block"));
+      if ((rc = bote_sweep_result_device(sh[i].sw, sh[i].local.p, sh[i].st))) return cleanup(rc);
+      if (hipMemcpyPeerAsync(dst, root, sh[i].local.p, dev, nb, sh[i].st) != hipSuccess)
+        return cleanup(fail(BOTE_E_DEVICE, "peer copy of a shard result"));
+    }
+    (void)hipSetDevice(dev);
+    if (hipEventRecord(sh[i].done, sh[i].st) != hipSuccess) return cleanup(fail(BOTE_E_DEVICE, "record shard event"));
+  }
+  HIP_TRY(hipSetDevice(root));
+  for (uint32_t i = 0; i < n_devices; ++i)
+    if (hipStreamWaitEvent(rst, sh[i].done, 0) != hipSuccess) return cleanup(fail(BOTE_E_DEVICE, "wait shard"));
+  // merge tree, at most 8 blocks per merge
+  const char* src = gathered.as<char>();
+  uint32_t m = n_devices;
+  char* bufs[2] = {bufa.as<char>(), bufb.as<char>()};
+  int bsel = 0;
+  while (m > (uint32_t)bote::G_MERGE_LISTS) {
+    const uint32_t groups = (m + bote::G_MERGE_LISTS - 1) / bote::G_MERGE_LISTS;
+    for (uint32_t g = 0; g < groups; ++g) {
+      const uint32_t k = std::min<uint32_t>(bote::G_MERGE_LISTS, m - bote::G_MERGE_LISTS * g);
+      if ((rc = bote_merge_device(sh[0].sw, src + (size_t)nb * bote::G_MERGE_LISTS * g, k, bufs[bsel] + (size_t)nb * g,
+                                  rst)))
+        return cleanup(rc);
+    }
+    src = bufs[bsel];
+    bsel ^= 1;
+    m = groups;
+  }
+  if ((rc = bote_merge_device(sh[0].sw, src, m, merged.p, rst))) return cleanup(rc);
+  std::vector<uint8_t> blk(nb);
+  HIP_TRY(hipMemcpyAsync(blk.data(), merged.p, nb, hipMemcpyDeviceToHost, rst));
+  HIP_TRY(hipStreamSynchronize(rst));
+  unpack_result(sh[0].sw, blk, out, out_count, out_valid, out_digest);
+  return cleanup(BOTE_OK);
 }
 
 }  // extern "C"

@@ -43,7 +43,7 @@ __device__ __forceinline__ bool finish_config(const FastArgs& a, const Mom (&mom
   bool amb = false;
   bool valid = false;
   const int fcap = min(N / 2, a.ft_metric);
-  if (a.want_score && !(a.ablate & 8)) {
+  if (a.want_score && !ABLATE(a, 8)) {
     valid = true;
 #pragma unroll
     for (int f = 1; f <= 2; ++f) {
@@ -79,7 +79,7 @@ __device__ __forceinline__ bool finish_config(const FastArgs& a, const Mom (&mom
   }
   if (amb) return false;
   if (valid) ++valid_cnt;
-  if (a.want_digest && !(a.ablate & 16)) {
+  if (a.want_digest && !ABLATE(a, 16)) {
     uint32_t h = 0;
 #pragma unroll
     for (int sl = 0; sl < NSLOT; ++sl)

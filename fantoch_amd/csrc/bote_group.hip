@@ -450,7 +450,7 @@ __global__ void __launch_bounds__(FAST_BD, BOTE_GROUP_WAVES) sweep_group_kernel(
             }
 #pragma unroll
             for (int k = N - 1; k < PV; ++k) v[k] = 0xFFFFFFFFu;
-            if (!(a.ablate & 32)) sort_network_pk<PV>(v);
+            if (!ABLATE(a, 32)) sort_network_pk<PV>(v);
             emit_pk(0, true, v);
           }
           {
@@ -461,7 +461,7 @@ __global__ void __launch_bounds__(FAST_BD, BOTE_GROUP_WAVES) sweep_group_kernel(
             for (int k = 0; k < F; ++k) v[2 + k] = l16(rqt + freg[k] * rstride + 2 * rv[2]) >> LAT_SHIFT;
 #pragma unroll
             for (int k = N - 1; k < PV; ++k) v[k] = 0xFFFFu;
-            if (!(a.ablate & 32)) sort_network<PV>(v);
+            if (!ABLATE(a, 32)) sort_network<PV>(v);
             emit_pk(2, false, v);
           }
           // ---- fixed rows (pairs): insert the 3 lane distances into the
@@ -474,7 +474,7 @@ __global__ void __launch_bounds__(FAST_BD, BOTE_GROUP_WAVES) sweep_group_kernel(
             const bool has_hi = 2 * pp + 1 < F;
 #pragma unroll
             for (int m = 0; m < 3; ++m) {
-              if (a.ablate & 64) break;
+              if (ABLATE(a, 64)) break;
               const uint32_t lo = l16(cv[m] + 2 * freg[2 * pp]);
               const uint32_t hi = has_hi ? l16(cv[m] + 2 * freg[has_hi ? 2 * pp + 1 : 2 * pp]) : 0xFFF0u;
               us2 x = as_us2((lo | (hi << 16)) >> LAT_SHIFT);
@@ -499,7 +499,7 @@ __global__ void __launch_bounds__(FAST_BD, BOTE_GROUP_WAVES) sweep_group_kernel(
           // closer call re-runs the scan exactly (cov2_sign) or defers.
           uint32_t bi = 0;
           bool amb = false;
-          if (!(a.ablate & 128)) {
+          if (!ABLATE(a, 128)) {
             float rl[N];
 #pragma unroll
             for (int l = 0; l < N; ++l) {
@@ -615,7 +615,7 @@ __global__ void __launch_bounds__(FAST_BD, BOTE_GROUP_WAVES) sweep_group_kernel(
                   s2[t] = 0;
                 }
               };
-              const uint32_t nql = (a.ablate & 1) ? 0u : nq;
+              const uint32_t nql = ABLATE(a, 1) ? 0u : nq;
               // 4 quads per iteration (constant offsets fold into the ds_read
               // offset fields); s2 is flushed to 64 bits every s2_flush quads
               {
@@ -640,11 +640,11 @@ __global__ void __launch_bounds__(FAST_BD, BOTE_GROUP_WAVES) sweep_group_kernel(
                   flush();
                 }
               }
-              if (rem && !(a.ablate & 1)) {
+              if (rem && !ABLATE(a, 1)) {
                 quad(nq * 8, rem >= 2 ? ~0u : 0x0000FFFFu, rem == 3 ? 0x0000FFFFu : 0u);
                 flush();
               }
-              if (a.ablate & 1) {  // timing only: non-degenerate dummy sums
+              if (ABLATE(a, 1)) {  // timing only: non-degenerate dummy sums
 #pragma unroll
                 for (int t = 0; t < NL; ++t) {
                   S1[t] = 1000u + rv[0] + t;
@@ -668,7 +668,7 @@ __global__ void __launch_bounds__(FAST_BD, BOTE_GROUP_WAVES) sweep_group_kernel(
               uint32_t sv = 0, sv2 = 0;
 #pragma unroll
               for (int k = 0; k < N; ++k) {
-                if (a.ablate & 512) break;
+                if (ABLATE(a, 512)) break;
                 const uint32_t v = l16(lcol + 2 * reg_of(k)) >> LAT_SHIFT;
                 sv += v;
                 sv2 += v * v;
@@ -690,7 +690,7 @@ __global__ void __launch_bounds__(FAST_BD, BOTE_GROUP_WAVES) sweep_group_kernel(
               bool valid = false;
               const int fcap = min(N / 2, a.ft_metric);
               bool defer = false;
-              if (a.want_score && !(a.ablate & 256)) {
+              if (a.want_score && !ABLATE(a, 256)) {
                 valid = true;
 #pragma unroll
                 for (int f = 1; f <= 2; ++f) {
@@ -732,7 +732,7 @@ __global__ void __launch_bounds__(FAST_BD, BOTE_GROUP_WAVES) sweep_group_kernel(
                 defer_rank(a, rank);
               } else {
                 if (valid) ++valid_cnt;
-                if (a.want_digest && !(a.ablate & 16)) {
+                if (a.want_digest && !ABLATE(a, 16)) {
                   uint32_t h = 0;
 #pragma unroll
                   for (int sl = 0; sl < NSLOT; ++sl) h = digest_fold(h, mom[sl].s1, mom[sl].s2);
@@ -802,7 +802,7 @@ __global__ void __launch_bounds__(FAST_BD, BOTE_GROUP_WAVES) sweep_group_kernel(
           }
         }
         // ---- top-K: lock-free screen, exact merge under the block lock
-        if (!(a.ablate & 4)) {
+        if (!ABLATE(a, 4)) {
           const int nobj = DEF ? 5 : a.n_obj;
           bool pass = false;
 #pragma unroll

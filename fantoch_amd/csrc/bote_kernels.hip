@@ -370,6 +370,7 @@ __global__ void __launch_bounds__(256) eval_kernel(EvalArgs a) {
   using QC = QCfg<N>;
   constexpr int NLW = QC::NL <= 2 ? 1 : 2;
   extern __shared__ __align__(16) unsigned char smem[];
+  if (a.run_if_over && *a.run_if_over <= a.over_cap) return;  // block-uniform, before any barrier
   const Smem s = carve<N>(a, smem, NLW);
   const uint32_t BD = blockDim.x, tid = threadIdx.x;
   const bool topk = !FULL && a.out_top != nullptr;
@@ -504,7 +505,12 @@ __global__ void __launch_bounds__(256) eval_kernel(EvalArgs a) {
 // lower list index).  One pass of binary searches in LDS, no sort; a block
 // that finds an unsorted input falls back to the full bitonic sort.
 __global__ void __launch_bounds__(256) merge_kernel(const Rec* src, uint32_t n_lists, uint64_t list_stride, Rec* dst,
-                                                     uint64_t out_stride) {
+                                                     uint64_t out_stride, const Rec* alt, uint32_t alt_lists,
+                                                     const unsigned long long* sel, uint64_t cap) {
+  if (sel && *sel > cap) {  // device-side choice of the input (fast sweep overflow fallback)
+    src = alt;
+    n_lists = alt_lists;
+  }
   __shared__ Rec buf[G_MERGE_LISTS * KP];
   __shared__ int unsorted;
   const uint32_t g = blockIdx.x, o = blockIdx.y;
@@ -680,7 +686,30 @@ hipError_t launch_eval(const EvalArgs& a, uint32_t n, bool full, uint32_t grid, 
 hipError_t launch_merge(const Rec* src, uint32_t n_lists, uint64_t list_stride, Rec* dst, uint64_t out_stride,
                         uint32_t n_obj, hipStream_t st) {
   uint32_t groups = (n_lists + G_MERGE_LISTS - 1) / G_MERGE_LISTS;
-  hipLaunchKernelGGL(merge_kernel, dim3(groups, n_obj), dim3(256), 0, st, src, n_lists, list_stride, dst, out_stride);
+  hipLaunchKernelGGL(merge_kernel, dim3(groups, n_obj), dim3(256), 0, st, src, n_lists, list_stride, dst, out_stride,
+                     (const Rec*)nullptr, 0u, (const unsigned long long*)nullptr, (uint64_t)0);
+  return hipGetLastError();
+}
+
+hipError_t launch_merge_sel(const Rec* src, uint32_t n_lists, const Rec* alt, uint32_t alt_lists, uint64_t list_stride,
+                            const unsigned long long* sel, uint64_t cap, Rec* dst, uint64_t out_stride, uint32_t n_obj,
+                            hipStream_t st) {
+  // groups cover the larger input; the surplus groups emit all-padding lists
+  const uint32_t m = n_lists > alt_lists ? n_lists : alt_lists;
+  uint32_t groups = (m + G_MERGE_LISTS - 1) / G_MERGE_LISTS;
+  hipLaunchKernelGGL(merge_kernel, dim3(groups, n_obj), dim3(256), 0, st, src, n_lists, list_stride, dst, out_stride,
+                     alt, alt_lists, sel, cap);
+  return hipGetLastError();
+}
+
+__global__ void pick_counters_kernel(const unsigned long long* src, const unsigned long long* alt,
+                                     const unsigned long long* sel, uint64_t cap, uint64_t* dst) {
+  if (threadIdx.x < 2) dst[threadIdx.x] = (*sel > cap ? alt : src)[threadIdx.x];
+}
+
+hipError_t launch_pick_counters(const unsigned long long* src, const unsigned long long* alt,
+                                const unsigned long long* sel, uint64_t cap, uint64_t* dst, hipStream_t st) {
+  hipLaunchKernelGGL(pick_counters_kernel, dim3(1), dim3(64), 0, st, src, alt, sel, cap, dst);
   return hipGetLastError();
 }
 

@@ -50,6 +50,11 @@ struct EvalArgs {
   Rec* out_top;                      // [grid][n_obj][KP]
   unsigned long long* out_counters;  // [0] valid count, [1] digest
   int want_digest;
+  // overflow fallback of the fast sweep: when set, every block exits at once
+  // unless *run_if_over > over_cap (the deferred-rank queue overflowed), so the
+  // fallback is stream-ordered with no host round trip
+  const unsigned long long* run_if_over;
+  uint64_t over_cap;
 };
 
 struct SingleArgs {
@@ -101,12 +106,21 @@ struct FastArgs {
   uint64_t* queue;  // deferred near-tie configs (colex ranks)
   unsigned long long* queue_count;
   uint64_t queue_cap;
-  // timing diagnostics only (env BOTE_ABLATE; results are wrong when set):
+#ifdef BOTE_ABLATION
+  // Timing-diagnostics builds only (scripts/build_variant.sh NAME -DBOTE_ABLATION,
+  // env BOTE_ABLATE; results are wrong when set).  The product library is
+  // compiled without it: ABLATE() is the constant false there.
   // 1 skip client loop, 2 skip Q phase, 4 skip top-K step, 8 skip score, 16 skip digest;
   // group kernel: 32 skip variable-row sorts, 64 skip fixed-row insertions,
   // 128 skip leader selection, 256 skip validity, 512 skip colocated FPaxos
   uint32_t ablate;
+#endif
 };
+#ifdef BOTE_ABLATION
+#define ABLATE(a, bit) (((a).ablate & (bit)) != 0)
+#else
+#define ABLATE(a, bit) false
+#endif
 size_t fast_smem_bytes(const FastArgs& a, uint32_t n);
 int fast_occupancy(uint32_t n, size_t shm);
 hipError_t launch_fast(const FastArgs& a, uint32_t n, uint32_t grid, size_t shm, hipStream_t st);
@@ -120,6 +134,14 @@ hipError_t launch_eval(const EvalArgs& a, uint32_t n, bool full, uint32_t grid, 
                        hipStream_t st);
 hipError_t launch_merge(const Rec* src, uint32_t n_lists, uint64_t list_stride, Rec* dst, uint64_t out_stride,
                         uint32_t n_obj, hipStream_t st);
+// Merge whose input is chosen on the device: `alt` (alt_lists lists) when
+// *sel > cap, else `src` (n_lists lists).
+hipError_t launch_merge_sel(const Rec* src, uint32_t n_lists, const Rec* alt, uint32_t alt_lists, uint64_t list_stride,
+                            const unsigned long long* sel, uint64_t cap, Rec* dst, uint64_t out_stride, uint32_t n_obj,
+                            hipStream_t st);
+// dst[0..1] = (*sel > cap ? alt : src)[0..1]
+hipError_t launch_pick_counters(const unsigned long long* src, const unsigned long long* alt,
+                                const unsigned long long* sel, uint64_t cap, uint64_t* dst, hipStream_t st);
 
 hipError_t launch_sum_counters(const uint64_t* src, uint32_t n, uint64_t stride, uint64_t off, uint64_t* dst,
                                hipStream_t st);

@@ -338,7 +338,7 @@ __global__ void __launch_bounds__(FAST_BD, 4) sweep_fast_kernel(FastArgs a) {
         for (int j = 0; j < N; ++j) {
           uint32_t v[P];
           int t = 0;
-          if (a.ablate & 2) {
+          if (ABLATE(a, 2)) {
 #pragma unroll
             for (int k = 0; k < N; ++k)
               if (k != j) v[t++] = colR[k] + rowq[j] + k;
@@ -408,9 +408,9 @@ __global__ void __launch_bounds__(FAST_BD, 4) sweep_fast_kernel(FastArgs a) {
           {
             uint32_t S1[NL];
             uint64_t S2[NL];
-            client_quads<N, NL>(B, s.cqt, (a.ablate & 1) ? 0u : nq, (a.ablate & 1) ? 0u : rem, a.s2_flush, colT,
+            client_quads<N, NL>(B, s.cqt, ABLATE(a, 1) ? 0u : nq, ABLATE(a, 1) ? 0u : rem, a.s2_flush, colT,
                                 qlane, S1, S2);
-            if (a.ablate & 1) {  // timing only: non-degenerate dummy sums (nothing defers)
+            if (ABLATE(a, 1)) {  // timing only: non-degenerate dummy sums (nothing defers)
 #pragma unroll
               for (int t = 0; t < NL; ++t) {
                 S1[t] = 1000u + colT[0] + t;
@@ -449,7 +449,7 @@ __global__ void __launch_bounds__(FAST_BD, 4) sweep_fast_kernel(FastArgs a) {
           }
         }
       }
-      if (!(a.ablate & 4)) topk_step(s.tk, a.n_obj, a.K, key, ok, rank);
+      if (!ABLATE(a, 4)) topk_step(s.tk, a.n_obj, a.K, key, ok, rank);
       if (jobok && rank < a.re) colex_next<N>(a.ns, p);
       ++rank;
     }

@@ -20,21 +20,33 @@ def shard_range(total: int, world: int, rank: int) -> Tuple[int, int]:
     return total * rank // world, total * (rank + 1) // world
 
 
-def sharded_sweep(sweep, stream=None, group=None, device: str = "cuda"):
+def _device_of(sweep, device):
+    """The torch device of the sweep's planet (a Sweep), unless given."""
+    import torch
+
+    if device is not None:
+        return torch.device(device)
+    dp = getattr(sweep, "dp", None)
+    return torch.device("cuda", dp.device) if dp is not None else torch.device("cuda")
+
+
+def sharded_sweep(sweep, stream=None, group=None, device=None):
     """Run `sweep` (fantoch_amd.bote.Sweep) over this rank's shard and return
     the merged result of all ranks (every rank gets the same result).
 
     `sweep` provides launch(rb, re, stream), result_bytes(),
     result_device(ptr, stream), merge_device(src_ptr, n, dst_ptr, stream) and
-    parse_block(np.ndarray); the blocks live on `device`."""
+    parse_block(np.ndarray); the blocks live on `device` (default: the GPU of
+    the sweep's planet, whose current stream is used)."""
     import torch
     import torch.distributed as dist
 
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     rank = dist.get_rank(group) if dist.is_initialized() else 0
     b, e = shard_range(sweep.total, world, rank)
-    if stream is None and device == "cuda":
-        stream = torch.cuda.current_stream().cuda_stream
+    device = _device_of(sweep, device)
+    if stream is None and device.type == "cuda":
+        stream = torch.cuda.current_stream(device).cuda_stream
     sweep.launch(b, e, stream)
     nbytes = sweep.result_bytes()
     blk = torch.empty(nbytes, dtype=torch.uint8, device=device)
@@ -46,11 +58,12 @@ def sharded_sweep(sweep, stream=None, group=None, device: str = "cuda"):
     return merge_gathered(sweep, gathered, world, stream, device)
 
 
-def merge_gathered(sweep, gathered, world: int, stream=None, device: str = "cuda"):
+def merge_gathered(sweep, gathered, world: int, stream=None, device=None):
     """Deterministic merge of `world` concatenated result blocks (the all-gather
     output, rank order) into one result; every rank runs it on its own copy."""
     import torch
 
+    device = _device_of(sweep, device)
     nbytes = sweep.result_bytes()
     out = torch.empty(nbytes, dtype=torch.uint8, device=device)
     # merge_device takes at most 8 blocks per call: a tree for larger worlds

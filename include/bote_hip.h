@@ -69,6 +69,12 @@ extern "C" {
 #define BOTE_OBJ_MEAN 1  /* min Histogram::mean of `slot` (exact sum order)          */
 #define BOTE_OBJ_COV 2   /* min Histogram::cov of `slot`, keyed fl64(V / S1^2)        */
 
+/* Sweep kernel paths (bote_sweep_create_ex); every path is exact. */
+#define BOTE_KERNEL_AUTO 0    /* group kernel when eligible, else fast, else generic */
+#define BOTE_KERNEL_GENERIC 1 /* eval_kernel (bote_kernels.hip): any planet */
+#define BOTE_KERNEL_FAST 2    /* sweep_fast_kernel (bote_sweep.hip) */
+#define BOTE_KERNEL_GROUP 3   /* sweep_group_kernel (bote_group.hip), n >= 4 */
+
 #define BOTE_FT_F1 1   /* FTMetric::F1   (search.rs:652-666) */
 #define BOTE_FT_F1F2 2 /* FTMetric::F1F2 */
 
@@ -121,6 +127,9 @@ int bote_quorum_size(int protocol, uint32_t n, uint32_t f);
 uint32_t bote_max_f(uint32_t n);
 
 /* ---------------------------------------------- Bote, one configuration --- */
+/* The per-call entry points below run stream-ordered on the planet's own
+ * HIP stream with cached device workspaces and synchronise only that stream;
+ * calls on one planet handle are serialised, distinct handles are independent. */
 /* Bote::quorum_latency (lib.rs:155-163) for every `from` in `froms`. */
 int bote_quorum_latencies(const bote_planet* p, const uint32_t* froms, uint32_t nf,
                           const uint32_t* regions, uint32_t nr, uint32_t q, uint64_t* out);
@@ -182,6 +191,15 @@ int bote_sweep_create(const bote_planet* p, const uint32_t* servers, uint32_t ns
                       const uint32_t* clients, uint32_t nc, uint32_t n,
                       const bote_objective* objs, uint32_t n_obj, uint32_t K,
                       const bote_ranking_params* rp, int digest, bote_sweep** out);
+/* bote_sweep_create with an explicit kernel path (BOTE_KERNEL_*); a forced
+ * fast/group path that the planet or lists do not qualify for is BOTE_E_ARG. */
+int bote_sweep_create_ex(const bote_planet* p, const uint32_t* servers, uint32_t ns,
+                         const uint32_t* clients, uint32_t nc, uint32_t n,
+                         const bote_objective* objs, uint32_t n_obj, uint32_t K,
+                         const bote_ranking_params* rp, int digest, int kernel, bote_sweep** out);
+/* Asynchronous on `hip_stream`: the sweep kernel, the exact fix-up of its
+ * deferred near-tie configs, the (device-decided) overflow fallback and the
+ * merge chain are all stream-ordered; no host synchronisation. */
 int bote_sweep_launch(bote_sweep* s, uint64_t rank_begin, uint64_t rank_end, void* hip_stream);
 int bote_sweep_result(bote_sweep* s, void* hip_stream, bote_topk_record* out, uint32_t* out_count,
                       uint64_t* out_valid, uint64_t* out_digest);
@@ -209,6 +227,22 @@ int bote_sweep_is_fast(const bote_sweep* s, int* out);
 /* Launch geometry chosen at creation (persistent grid, block size, LDS bytes). */
 int bote_sweep_grid(const bote_sweep* s, uint32_t* out_grid, uint32_t* out_block, uint32_t* out_lds_bytes);
 int bote_sweep_destroy(bote_sweep* s);
+
+/* ------------------------------------------ multi-device search (one call) --- */
+/* The exhaustive search over colex ranks [rank_begin, rank_end) sharded over
+ * n_devices planets (planets[i] lives on the device that sweeps shard i; a
+ * device may appear more than once).  Shards run concurrently, one HIP stream
+ * each; their result blocks are peer-copied to planets[0]'s device and merged
+ * there by (key, rank).  Outputs as bote_sweep_result; the result equals one
+ * unsharded sweep.  Replaces the rayon fork-join of Search::compute_all_configs
+ * (search.rs:199-232) for a single client set.  Every planet must hold the
+ * same latency matrix. */
+int bote_search_topk(const bote_planet* const* planets, uint32_t n_devices,
+                     const uint32_t* servers, uint32_t ns, const uint32_t* clients, uint32_t nc,
+                     uint32_t n, uint64_t rank_begin, uint64_t rank_end,
+                     const bote_objective* objs, uint32_t n_obj, uint32_t K,
+                     const bote_ranking_params* rp, int digest, bote_topk_record* out,
+                     uint32_t* out_count, uint64_t* out_valid, uint64_t* out_digest);
 
 /* colex unrank helper (host): rank -> n ascending positions < ns. */
 int bote_colex_unrank(uint64_t rank, uint32_t n, uint32_t ns, uint32_t* out_positions);

@@ -17,6 +17,7 @@ import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CONFIGS = {"r64n7": 621216192, "r128n6": 5423611200}
 
 
 def main():
@@ -49,6 +50,7 @@ def main():
         i += 1
     out.append("\n## PMC per dispatch (separate `--pmc` passes, averaged over dispatches)\n")
     traffic = None
+    pmc = {}
     for k, cs in counters.items():
         if "sweep" not in k and "eval_kernel" not in k:
             continue
@@ -70,8 +72,30 @@ def main():
         if k == dominant and "FETCH_SIZE" in per and "WRITE_SIZE" in per:
             traffic = (per["FETCH_SIZE"] + per["WRITE_SIZE"]) * 1024.0
             out.append(f"HBM traffic per launch (FETCH_SIZE + WRITE_SIZE, KiB -> bytes): {traffic:.4g} B")
+        if k == dominant and "SQ_INSTS_VALU" in per:
+            cfgs = CONFIGS.get(wl.split("_")[0])
+            kns = next((float(r["AverageNs"]) for r in rows if r["Name"] == k), None)
+            if cfgs and kns:
+                lanes = cfgs / 64.0
+                # GRBM_GUI_ACTIVE is summed over the 8 XCDs
+                clk = per["GRBM_GUI_ACTIVE"] / kns / 8 if "GRBM_GUI_ACTIVE" in per else 2.4
+                util = per["SQ_INSTS_VALU"] * 2 / (1024 * kns * clk)
+                pmc[wl] = {"valu_insts_per_config": per["SQ_INSTS_VALU"] / lanes,
+                           "lds_insts_per_config": per.get("SQ_INSTS_LDS", 0) / lanes,
+                           "salu_insts_per_config": per.get("SQ_INSTS_SALU", 0) / lanes,
+                           "clock_ghz": clk, "kernel_ns": kns, "valu_issue_util": util,
+                           "source": f"profiles/{tag}_profile.md"}
+                out.append(f"VALU wave-instructions per config: {pmc[wl]['valu_insts_per_config']:.1f} "
+                           f"(LDS {pmc[wl]['lds_insts_per_config']:.1f}, SALU {pmc[wl]['salu_insts_per_config']:.1f}); "
+                           f"VALU issue utilisation (SQ_INSTS_VALU x 2 cyc / (1024 SIMD x cycles) at "
+                           f"{clk:.2f} GHz): {util:.1%}")
         out.append("")
     open(os.path.join(ROOT, "profiles", f"{tag}_profile.md"), "w").write("\n".join(out) + "\n")
+    if pmc:
+        p = os.path.join(ROOT, "profiles", "pmc.json")
+        d = json.load(open(p)) if os.path.exists(p) else {}
+        d.update(pmc)
+        json.dump(d, open(p, "w"), indent=1, sort_keys=True)
     if traffic is not None:
         p = os.path.join(ROOT, "profiles", "traffic.json")
         d = json.load(open(p)) if os.path.exists(p) else {}

@@ -1,0 +1,118 @@
+"""GPU tests of the C-ABI boundary added for SURVEY.md §8b: the one-call
+multi-device search (bote_search_topk), the device-side overflow fallback of
+the fast sweep (no host round trip per launch) and the stream-ordered per-call
+entry points (reentrant across planet handles)."""
+import json
+import os
+import threading
+
+import numpy as np
+import pytest
+
+import oracle as O
+from fantoch_amd import _lib
+from fantoch_amd.bote import DEFAULT_OBJECTIVES, DEFAULT_RANKING, Bote, DevicePlanet, Sweep, search_topk
+from fantoch_amd.planet import Planet
+
+pytestmark = pytest.mark.gpu
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def _same(a, b):
+    return (a.valid, a.digest, a.tops) == (b.valid, b.digest, b.tops)
+
+
+def test_search_topk_shards_equal_unsharded():
+    """devices = [0, 0, 0] (and 9 shards, a two-level merge tree): identical to
+    one unsharded sweep of the same rank range."""
+    p = Planet.synthetic(64)
+    dp = DevicePlanet(p)
+    srv = np.arange(64, dtype=np.uint32)
+    rb, re = 300_000_000, 330_000_000
+    sw = Sweep(dp, srv, srv, 7, DEFAULT_OBJECTIVES, K=100, ranking=DEFAULT_RANKING, digest=True)
+    sw.launch(rb, re)
+    full = sw.result()
+    assert _same(search_topk([dp], srv, srv, 7, rank_begin=rb, rank_end=re), full)
+    three = [DevicePlanet(p) for _ in range(3)]  # distinct handles on one device
+    assert _same(search_topk(three, srv, srv, 7, rank_begin=rb, rank_end=re), full)
+    assert _same(search_topk([dp] * 9, srv, srv, 7, rank_begin=rb, rank_end=re), full)
+
+
+def test_search_topk_full_r64n7_vs_oracle_fixture():
+    """The bench workload in full through bote_search_topk with 3 shards on
+    device 0, against the oracle's full sweep (tests/golden/syn_r64n7_full.json)."""
+    path = os.path.join(GOLDEN, "syn_r64n7_full.json")
+    if not os.path.exists(path):
+        pytest.skip("fixture not generated yet (scripts/oracle_fixtures.sh)")
+    fx = json.load(open(path))
+    p = Planet.synthetic(64)
+    dps = [DevicePlanet(p) for _ in range(3)]
+    srv = np.arange(64, dtype=np.uint32)
+    got = search_topk(dps, srv, srv, 7)
+    assert (got.valid, got.digest) == (fx["valid"], fx["digest"])
+    assert got.tops == [[tuple(r) for r in t] for t in fx["tops"]]
+
+
+def test_overflow_fallback_is_device_side():
+    """A planet whose configs all defer (more than the 2^20-entry queue): the
+    generic fallback is chosen on the device; result_device (no host sync in
+    the library) then a device merge equals the oracle."""
+    import torch
+
+    from fantoch_amd.dist import merge_gathered
+
+    regions, p = Planet.equidistant(7, 48)
+    dp = DevicePlanet(p)
+    o = O.OraclePlanet.of(p)
+    srv = np.arange(p.R, dtype=np.uint32)
+    total = _lib.binomial(p.R, 5)
+    tops, valid, digest = o.sweep(srv, srv, 5, 0, total, DEFAULT_OBJECTIVES, 100,
+                                  (110.0, 35.0, 0.0, 15.0), 2, 8)
+    sw = Sweep(dp, srv, srv, 5, DEFAULT_OBJECTIVES, K=100, ranking=DEFAULT_RANKING, digest=True, kernel="fast")
+    nb = sw.result_bytes()
+    g = torch.empty(2 * nb, dtype=torch.uint8, device="cuda")
+    stream = torch.cuda.current_stream().cuda_stream
+    half = total // 2
+    sw.launch(0, half, stream)
+    sw.result_device(g.data_ptr(), stream)
+    sw.launch(half, total, stream)
+    sw.result_device(g.data_ptr() + nb, stream)
+    got = merge_gathered(sw, g, 2)
+    assert (got.valid, got.digest) == (valid, digest)
+    assert got.tops == [list(t) for t in tops]
+    # and through the multi-device entry point
+    got2 = search_topk([dp, dp], srv, srv, 5)
+    assert (got2.valid, got2.digest, got2.tops) == (valid, digest, [list(t) for t in tops])
+
+
+def test_per_call_entries_concurrent_handles():
+    """Bote::leaderless / leader / best_leader from 4 threads, each on its own
+    planet handle (own stream and workspace), equal the oracle."""
+    p = Planet.new()
+    o = O.OraclePlanet.of(p)
+    errors = []
+
+    def worker(seed):
+        try:
+            b = Bote(p)
+            rng = np.random.default_rng(seed)
+            for _ in range(25):
+                ns = int(rng.integers(2, 12))
+                servers = rng.choice(p.R, ns, replace=False)
+                clients = rng.choice(p.R, int(rng.integers(1, 20)), replace=True)
+                q = int(rng.integers(1, ns + 1))
+                sv = [p.names[i] for i in servers]
+                cv = [p.names[i] for i in clients]
+                assert [v for _, v in b.leaderless(sv, cv, q)] == o.leaderless(servers, clients, q).tolist()
+                lead = int(rng.integers(0, p.R))
+                assert [v for _, v in b.leader(p.names[lead], sv, cv, q)] == o.leader(lead, servers, clients,
+                                                                                      q).tolist()
+        except Exception as e:  # surfaced below
+            errors.append(e)
+
+    th = [threading.Thread(target=worker, args=(s,)) for s in range(4)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errors, errors

@@ -360,16 +360,13 @@ def test_r128_n6_subrange_and_max_latency():
 
 # ------------------------------------------------ fast path vs generic ----
 def _sweep(dp, srv, cli, n, rb, re, K=100, ranking=DEFAULT_RANKING, generic=False, kernel=None):
-    """kernel: None (default choice), 'generic', 'fast' or 'group' (BOTE_SWEEP_KERNEL)."""
+    """kernel: None (default choice), 'generic', 'fast' or 'group' (bote_sweep_create_ex)."""
     kernel = "generic" if generic else kernel
+    if kernel == "group" and n < 4:
+        kernel = "fast"
+    sw = Sweep(dp, srv, cli, n, DEFAULT_OBJECTIVES, K=K, ranking=ranking, digest=True, kernel=kernel)
     if kernel:
-        os.environ["BOTE_SWEEP_KERNEL"] = kernel
-    try:
-        sw = Sweep(dp, srv, cli, n, DEFAULT_OBJECTIVES, K=K, ranking=ranking, digest=True)
-    finally:
-        os.environ.pop("BOTE_SWEEP_KERNEL", None)
-    if kernel:
-        assert sw.kernel_path() == (kernel if not (kernel == "group" and n < 4) else "fast")
+        assert sw.kernel_path() == kernel
     sw.launch(rb, re)
     return sw.result()
 
@@ -406,11 +403,7 @@ def test_group_kernel_custom_objectives():
             (_lib.OBJ_COV, 5 + _lib.SLOT_E), (_lib.OBJ_MEAN, _lib.SLOT_AF1), (_lib.OBJ_COV, _lib.SLOT_FF1)]
     out = {}
     for k in ("generic", "group"):
-        os.environ["BOTE_SWEEP_KERNEL"] = k
-        try:
-            sw = Sweep(dp, srv, srv, 7, objs, K=50, ranking=DEFAULT_RANKING, digest=True)
-        finally:
-            os.environ.pop("BOTE_SWEEP_KERNEL", None)
+        sw = Sweep(dp, srv, srv, 7, objs, K=50, ranking=DEFAULT_RANKING, digest=True, kernel=k)
         assert sw.kernel_path() == k
         sw.launch(200_000_000, 201_500_000)
         r = sw.result()
