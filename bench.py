@@ -253,7 +253,7 @@ def main():
                          "survey_w": W, "survey_w_frac": shard * W / (kavg_ms * 1e-3) / 1e12 / VALU_PEAK_TOPS,
                          "valu_issue": valu, "kernel_ms_avg": kavg_ms,
                          "kernel": KERNEL_NAMES[sweep.kernel_path()]},
-            "result_check": {"valid": res.valid, "digest": res.digest,
+            "result_check": {"valid": res.valid, "digest": res.digest, "deferred": sweep.deferred(stream),
                              "top_score_rank": res.tops[0][0][1] if res.tops[0] else None, "fixture": check},
         }
         if os.environ.get("BOTE_LIB_PATH"):

@@ -667,6 +667,12 @@ class Sweep:
         check(lib().bote_sweep_timing(self.h, C.byref(ms), C.byref(n)))
         return ms.value, n.value
 
+    def deferred(self, stream: Optional[int] = None) -> int:
+        """Configs the last launch deferred to the exact generic kernel."""
+        v = C.c_uint64()
+        check(lib().bote_sweep_deferred(self.h, C.c_void_p(stream) if stream else None, C.byref(v)))
+        return v.value
+
     def is_fast(self) -> bool:
         """True when a fast-path kernel (packed or group) runs the sweep."""
         return self.kernel_path() != "generic"

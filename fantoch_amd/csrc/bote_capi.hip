@@ -927,6 +927,18 @@ int bote_sweep_timing(bote_sweep* s, float* out_total_ms, uint32_t* out_launches
   return BOTE_OK;
 }
 
+int bote_sweep_deferred(bote_sweep* s, void* hip_stream, uint64_t* out) {
+  if (!s || !out) return fail(BOTE_E_ARG, "null argument");
+  *out = 0;
+  if (!s->fast || !s->launched) return BOTE_OK;
+  HIP_TRY(hipSetDevice(s->p->device));
+  unsigned long long q = 0;
+  HIP_TRY(hipMemcpyAsync(&q, s->qcount.p, 8, hipMemcpyDeviceToHost, (hipStream_t)hip_stream));
+  HIP_TRY(hipStreamSynchronize((hipStream_t)hip_stream));
+  *out = q;
+  return BOTE_OK;
+}
+
 int bote_sweep_grid(const bote_sweep* s, uint32_t* out_grid, uint32_t* out_block, uint32_t* out_lds_bytes) {
   if (!s) return fail(BOTE_E_ARG, "sweep is null");
   if (out_grid) *out_grid = s->fast ? s->fgrid : s->grid;

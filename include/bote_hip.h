@@ -224,6 +224,10 @@ int bote_sweep_timing(bote_sweep* s, float* out_total_ms, uint32_t* out_launches
  * packed fast-path kernel (bote_sweep.hip), 2 the group kernel
  * (bote_group.hip).  All are exact (DESIGN.md "Kernels"). */
 int bote_sweep_is_fast(const bote_sweep* s, int* out);
+/* Configs the fast/group kernel deferred to the exact generic kernel in the
+ * last launch (COV near-ties; more than 2^20 => the whole range was recomputed
+ * on the generic path).  Synchronises `hip_stream`.  0 on the generic path. */
+int bote_sweep_deferred(bote_sweep* s, void* hip_stream, uint64_t* out);
 /* Launch geometry chosen at creation (persistent grid, block size, LDS bytes). */
 int bote_sweep_grid(const bote_sweep* s, uint32_t* out_grid, uint32_t* out_block, uint32_t* out_lds_bytes);
 int bote_sweep_destroy(bote_sweep* s);

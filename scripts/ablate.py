@@ -1,6 +1,8 @@
 """Timing diagnostics: kernel time of the fast sweep with sections skipped
 (BOTE_ABLATE bit mask, see FastArgs::ablate).  Results are wrong when a bit is
-set; only the times matter."""
+set; only the times matter.  Needs a library built with -DBOTE_ABLATION
+(scripts/build_variant.sh abl -DBOTE_ABLATION; BOTE_LIB_PATH=fantoch_amd/lib_abl/...):
+the product library has no ablation switches."""
 import os
 import sys
 

@@ -7,6 +7,7 @@
 set -euo pipefail
 cd "$(dirname "$0")/.."
 T=${THREADS:-8}
+if [ ! -f tests/golden/syn_r128n6_windows.json ]; then
 for b in 0 3338380 49563860 300000200 1191552400 2141351635 3652245460 5168879425 5422611200; do
   python scripts/oracle_full_sweep.py --workload r128n6 --threads "$T" --chunk 1000000 \
     --rank-begin "$b" --rank-end $((b + 1000000)) --name "win_r128n6_$b"
@@ -20,4 +21,5 @@ for p in sorted(glob.glob("tests/golden/win_r128n6_*.json"), key=lambda p: int(p
 json.dump({"what": "oracle sweeps of 10^6-rank windows of the synthetic R=128 planet, n=6",
            "generator": "scripts/oracle_fixtures.sh", "windows": ws}, open("tests/golden/syn_r128n6_windows.json", "w"))
 EOF
+fi
 python scripts/oracle_full_sweep.py --workload r64n7 --threads "$T" --chunk 4194304
