@@ -142,6 +142,69 @@ def eval_configs(dp: DevicePlanet, servers: Sequence[int], clients: Sequence[int
     return EvalResult(n, nc, vals, lead, s1, s2, mean, cov, score, valid)
 
 
+@dataclass
+class LeaderlessResult:
+    """bote_eval_leaderless outputs: per config and quorum size."""
+    n: int
+    nc: int
+    quorum_sizes: List[int]
+    vals: Optional[np.ndarray]   # (ncfg, nq, nc + n) uint32: Input clients, then Colocated (config order)
+    s1: np.ndarray               # (ncfg, nq, 2) uint64: [Input, Colocated]
+    s2: np.ndarray               # (ncfg, nq, 2) uint64
+
+
+def eval_leaderless(dp: DevicePlanet, servers: Sequence[int], clients: Sequence[int], n: int,
+                    quorum_sizes: Sequence[int], configs: Optional[np.ndarray] = None, rank_begin: int = 0,
+                    ncfg: Optional[int] = None, values: bool = True) -> LeaderlessResult:
+    """`Bote::leaderless` (lib.rs:38-59) for a batch of configurations and up to
+    8 quorum sizes at once (Tempo's fast/tiny/write quorums, config.rs:317-329)."""
+    srv, cli, qs = u32(servers), u32(clients), u32(quorum_sizes)
+    if configs is not None:
+        cfg = np.ascontiguousarray(np.asarray(configs, dtype=np.uint32).reshape(-1, n))
+        ncfg = cfg.shape[0]
+        cptr = ptr(cfg)
+    else:
+        cfg, cptr = None, None
+        if ncfg is None:
+            ncfg = _lib.binomial(len(srv), n) - rank_begin
+    nc, nq = len(cli), len(qs)
+    vals = np.zeros((ncfg, nq, nc + n), np.uint32) if values else None
+    s1 = np.zeros((ncfg, nq, 2), np.uint64)
+    s2 = np.zeros((ncfg, nq, 2), np.uint64)
+    check(lib().bote_eval_leaderless(dp.h, srv, len(srv), cli, nc, n, cptr, rank_begin, ncfg, qs, nq, ptr(vals),
+                                     ptr(s1), ptr(s2)))
+    return LeaderlessResult(n, nc, [int(q) for q in qs], vals, s1, s2)
+
+
+def tempo_quorums(n: int) -> List[Tuple[Protocol, int, int]]:
+    """(protocol, f, quorum size) of Tempo's fast (non-tiny, tiny) and write
+    quorums for f = 1..max_f(n) (config.rs:317-329; max_f: search.rs:474-477)."""
+    out = []
+    for f in range(1, max_f(n) + 1):
+        for proto in (Protocol.Tempo, Protocol.TempoTiny, Protocol.TempoWrite):
+            out.append((proto, f, proto.quorum_size(n, f)))
+    return out
+
+
+def tempo_stats(dp: DevicePlanet, servers: Sequence[int], clients: Sequence[int], n: int,
+                configs: np.ndarray) -> List[ProtocolStats]:
+    """Tempo keys (`tf{f}`, `ttf{f}`, `twf{f}` and their `C` variants) for each
+    configuration, from the device (bote_eval_leaderless)."""
+    tq = tempo_quorums(n)
+    qs = sorted({q for _, _, q in tq})
+    r = eval_leaderless(dp, servers, clients, n, qs, configs=configs)
+    nc = len(u32(clients))
+    out = []
+    for i in range(r.vals.shape[0]):
+        st = ProtocolStats.new()
+        for proto, f, q in tq:
+            row = r.vals[i, qs.index(q)]
+            st.insert(proto, f, ClientPlacement.Input, Histogram.from_values(row[:nc].tolist()))
+            st.insert(proto, f, ClientPlacement.Colocated, Histogram.from_values(row[nc:].tolist()))
+        out.append(st)
+    return out
+
+
 # ----------------------------------------------------------------- Bote ---
 class Bote:
     """lib.rs:16-186 — the analytic latency model over a device planet."""
@@ -407,13 +470,17 @@ class Search:
         return ConfigAndStats([Region(self.planet.names[r]) for r in ids], mask, self, (ci, n, i))
 
     @staticmethod
-    def compute_stats(config: Sequence, all_clients: Sequence, bote: Bote) -> ProtocolStats:
-        """search.rs:262-319 for one configuration (config order = given order)."""
+    def compute_stats(config: Sequence, all_clients: Sequence, bote: Bote, tempo: bool = False) -> ProtocolStats:
+        """search.rs:262-319 for one configuration (config order = given order).
+        tempo=True adds Tempo's keys (tempo_stats; BASELINE config 2)."""
         srv = bote.planet.idxs(config)
         cli = bote.planet.idxs(all_clients)
         n = len(srv)
-        r = eval_configs(bote.dp, srv, cli, n, configs=np.arange(n, dtype=np.uint32).reshape(1, n))
-        return r.protocol_stats(0)
+        one = np.arange(n, dtype=np.uint32).reshape(1, n)
+        st = eval_configs(bote.dp, srv, cli, n, configs=one).protocol_stats(0)
+        if tempo:
+            st.map.update(tempo_stats(bote.dp, srv, cli, n, one)[0].map)
+        return st
 
     # ------------------------------------------------------------ ranking ---
     def _rank(self, configs: Dict[int, dict], p: RankingParams, ci: int):

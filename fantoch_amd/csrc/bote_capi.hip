@@ -516,6 +516,89 @@ int bote_eval(const bote_planet* p, const uint32_t* servers, uint32_t ns, const 
   return BOTE_OK;
 }
 
+// ------------------------------------------ leaderless, many quorum sizes
+// Bote::leaderless (lib.rs:38-59) over a batch of configurations for each of
+// `nq` quorum sizes: Tempo's fast (n/2 + f; tiny 2f) and write (f + 1)
+// quorums (fantoch/src/config.rs:317-329), which compute_stats does not key.
+int bote_eval_leaderless(const bote_planet* p, const uint32_t* servers, uint32_t ns, const uint32_t* clients,
+                         uint32_t nc, uint32_t n, const uint32_t* configs, uint64_t rank_begin, uint64_t ncfg,
+                         const uint32_t* quorum_sizes, uint32_t nq, uint32_t* out_vals, uint64_t* out_sum,
+                         uint64_t* out_sumsq) {
+  int rc;
+  if (!p) return fail(BOTE_E_ARG, "planet is null");
+  if (n < 1 || n > BOTE_MAX_N) return fail(BOTE_E_RANGE, "config size must be in [1, 16]");
+  if (n > ns) return fail(BOTE_E_ARG, "config size larger than the server list");
+  if (nc > BOTE_MAX_CLIENTS) return fail(BOTE_E_RANGE, "more than 4096 clients");
+  if (nq == 0 || nq > 8 || !quorum_sizes) return fail(BOTE_E_ARG, "1 to 8 quorum sizes");
+  for (uint32_t i = 0; i < nq; ++i) {
+    if (quorum_sizes[i] == 0) return fail(BOTE_E_ARG, "quorum size 0");
+    if (quorum_sizes[i] > n) return fail(BOTE_E_QUORUM_GT_N, "quorum larger than the config");
+  }
+  if ((rc = check_regions(servers, ns, p->R, true, "servers"))) return rc;
+  if ((rc = check_regions(clients, nc, p->R, false, "clients"))) return rc;
+  if (ncfg == 0) return BOTE_OK;
+  if (configs) {
+    for (uint64_t i = 0; i < ncfg; ++i) {
+      uint32_t seen[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      for (uint32_t j = 0; j < n; ++j) {
+        uint32_t x = configs[i * n + j];
+        if (x >= ns) return fail(BOTE_E_ARG, "config position out of range");
+        if (seen[x >> 5] & (1u << (x & 31))) return fail(BOTE_E_ARG, "duplicate position in config");
+        seen[x >> 5] |= 1u << (x & 31);
+      }
+    }
+  } else {
+    uint64_t total = binom_u64(ns, n);
+    if (rank_begin > total || ncfg > total - rank_begin) return fail(BOTE_E_ARG, "rank range out of bounds");
+  }
+  std::lock_guard<std::mutex> lk(p->mu);
+  HIP_TRY(hipSetDevice(p->device));
+  hipStream_t st = p->stream;
+  DBuf &ds = p->ws[0], &dc = p->ws[1], &dcfg = p->ws[2], &dbin = p->ws[3], &dq = p->ws[4], &dvals = p->ws[5],
+       &ds1 = p->ws[6], &ds2 = p->ws[7];
+  HIP_TRY(ds.reserve(ns * 4));
+  HIP_TRY(dc.reserve(nc * 4));
+  HIP_TRY(dq.reserve(nq * 4));
+  HIP_TRY(hipMemcpyAsync(ds.p, servers, ns * 4, hipMemcpyHostToDevice, st));
+  if (nc) HIP_TRY(hipMemcpyAsync(dc.p, clients, nc * 4, hipMemcpyHostToDevice, st));
+  HIP_TRY(hipMemcpyAsync(dq.p, quorum_sizes, nq * 4, hipMemcpyHostToDevice, st));
+  bote::LqArgs a{};
+  a.mat = p->d_mat;
+  a.R = p->R;
+  a.srv = ds.as<uint32_t>();
+  a.ns = ns;
+  a.cli = dc.as<uint32_t>();
+  a.nc = nc;
+  a.qs = dq.as<uint32_t>();
+  a.nq = nq;
+  a.ncfg = ncfg;
+  std::vector<uint64_t> t;
+  if (configs) {
+    HIP_TRY(dcfg.reserve(ncfg * n * 4));
+    HIP_TRY(hipMemcpyAsync(dcfg.p, configs, ncfg * n * 4, hipMemcpyHostToDevice, st));
+    a.cfgs = dcfg.as<uint32_t>();
+  } else {
+    t = binom_table(ns, n);
+    HIP_TRY(dbin.reserve(t.size() * 8));
+    HIP_TRY(hipMemcpyAsync(dbin.p, t.data(), t.size() * 8, hipMemcpyHostToDevice, st));
+    a.binom = dbin.as<uint64_t>();
+    a.rank_begin = rank_begin;
+  }
+  const size_t nv = (size_t)ncfg * nq * (nc + n), nm = (size_t)ncfg * nq * 2;
+  if (out_vals) { HIP_TRY(dvals.reserve(nv * 4)); a.out_vals = dvals.as<uint32_t>(); }
+  if (out_sum) { HIP_TRY(ds1.reserve(nm * 8)); a.out_sum = ds1.as<uint64_t>(); }
+  if (out_sumsq) { HIP_TRY(ds2.reserve(nm * 8)); a.out_sumsq = ds2.as<uint64_t>(); }
+  const size_t shm = bote::lq_smem_bytes(a, n);
+  if (shm > device_max_lds(p->device)) return fail(BOTE_E_RANGE, "planet/client set too large for LDS");
+  const uint32_t grid = (uint32_t)std::min<uint64_t>((ncfg + 255) / 256, (uint64_t)device_cus(p->device) * 4);
+  HIP_TRY(bote::launch_leaderless_q(a, n, grid, shm, st));
+  if (out_vals) HIP_TRY(hipMemcpyAsync(out_vals, dvals.p, nv * 4, hipMemcpyDeviceToHost, st));
+  if (out_sum) HIP_TRY(hipMemcpyAsync(out_sum, ds1.p, nm * 8, hipMemcpyDeviceToHost, st));
+  if (out_sumsq) HIP_TRY(hipMemcpyAsync(out_sumsq, ds2.p, nm * 8, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  return BOTE_OK;
+}
+
 // ------------------------------------------------------------------ sweep
 int bote_sweep_create(const bote_planet* p, const uint32_t* servers, uint32_t ns, const uint32_t* clients,
                       uint32_t nc, uint32_t n, const bote_objective* objs, uint32_t n_obj, uint32_t K,

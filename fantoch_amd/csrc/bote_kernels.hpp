@@ -145,6 +145,26 @@ hipError_t launch_pick_counters(const unsigned long long* src, const unsigned lo
 
 hipError_t launch_sum_counters(const uint64_t* src, uint32_t n, uint64_t stride, uint64_t off, uint64_t* dst,
                                hipStream_t st);
+// ---- leaderless latencies for several quorum sizes (bote_quorums.hip)
+struct LqArgs {
+  const uint32_t* mat;  // latency << 4
+  uint32_t R;
+  const uint32_t* srv;
+  uint32_t ns;
+  const uint32_t* cli;
+  uint32_t nc;
+  const uint32_t* cfgs;  // ncfg x n positions, or null (colex ranks from rank_begin)
+  const uint64_t* binom;
+  uint64_t rank_begin, ncfg;
+  const uint32_t* qs;  // nq quorum sizes, each in [1, n]
+  uint32_t nq;
+  uint32_t* out_vals;   // ncfg x nq x (nc + n)
+  uint64_t* out_sum;    // ncfg x nq x 2 (Input, Colocated)
+  uint64_t* out_sumsq;  // ncfg x nq x 2
+};
+size_t lq_smem_bytes(const LqArgs& a, uint32_t n);
+hipError_t launch_leaderless_q(const LqArgs& a, uint32_t n, uint32_t grid, size_t shm, hipStream_t st);
+
 hipError_t launch_single(const SingleArgs& a, int mode, hipStream_t st);
 hipError_t launch_best_leader(const SingleArgs& a, const uint64_t* vals, double* stat, hipStream_t st);
 

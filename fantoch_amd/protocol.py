@@ -16,15 +16,16 @@ class Protocol(enum.Enum):
     FPaxos = 0
     EPaxos = 1
     Atlas = 2
-    Tempo = 3
-    TempoTiny = 4
+    Tempo = 3        # fast quorum, non-tiny: n/2 + f
+    TempoTiny = 4    # fast quorum, tiny: 2f
+    TempoWrite = 5   # write quorum: f + 1
 
     def short_name(self) -> str:
-        return {0: "f", 1: "e", 2: "a", 3: "t", 4: "tt"}[self.value]
+        return {0: "f", 1: "e", 2: "a", 3: "t", 4: "tt", 5: "tw"}[self.value]
 
     def quorum_size(self, n: int, f: int) -> int:
-        """protocol.rs:20-31; Tempo: config.rs:317-329 (fast quorum)."""
-        if self is Protocol.FPaxos:
+        """protocol.rs:20-31; Tempo: config.rs:317-329 (fast and write quorums)."""
+        if self is Protocol.FPaxos or self is Protocol.TempoWrite:
             return f + 1
         if self is Protocol.EPaxos:
             m = Protocol.minority(n)

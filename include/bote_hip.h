@@ -173,6 +173,20 @@ int bote_eval(const bote_planet* p, const uint32_t* servers, uint32_t ns,
               uint32_t* out_vals, uint32_t* out_leader, uint64_t* out_sum, uint64_t* out_sumsq,
               double* out_mean, double* out_cov, double* out_score, uint8_t* out_valid);
 
+/* Bote::leaderless (lib.rs:38-59) for a batch of configurations (as in
+ * bote_eval: `configs` or colex ranks) and nq quorum sizes (1..8, each <= n) at
+ * once.  This carries Tempo (fantoch/src/config.rs:317-329): fast quorum
+ * n/2 + f (tiny: 2f) and write quorum f + 1, which Search::compute_stats does
+ * not key.  Per config and quorum size (config-major, then quorum order):
+ *   out_vals   nc Input-client latencies (client order) then n Colocated
+ *              latencies (config order): ncfg x nq x (nc + n) uint32
+ *   out_sum, out_sumsq  exact sum / sum of squares, [Input, Colocated]:
+ *              ncfg x nq x 2 uint64 */
+int bote_eval_leaderless(const bote_planet* p, const uint32_t* servers, uint32_t ns,
+                         const uint32_t* clients, uint32_t nc, uint32_t n, const uint32_t* configs,
+                         uint64_t rank_begin, uint64_t ncfg, const uint32_t* quorum_sizes, uint32_t nq,
+                         uint32_t* out_vals, uint64_t* out_sum, uint64_t* out_sumsq);
+
 /* ------------------------------------------------ streaming search (hot) --- */
 /* The exhaustive sweep (search.rs:199-260 + compute_stats + compute_score)
  * over colex ranks [rank_begin, rank_end) of n-subsets of `servers`, keeping

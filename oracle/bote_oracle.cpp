@@ -21,6 +21,8 @@
 //    * compute_score / rank / super_configs /            fantoch_bote/src/search.rs:97-178,321-472
 //      min_mean_decrease / sorted_evolving_configs
 //    * FTMetric::fs, max_f                               fantoch_bote/src/search.rs:474-477,652-666
+//    * Tempo quorum sizes (fast n/2+f, tiny 2f, write f+1) fantoch/src/config.rs:317-329 (through
+//      Bote::leaderless, oracle_leaderless_batch)
 //
 //  Pinned against the reference's own known-answer tests (tests/test_oracle.py):
 //  lib.rs:193-465, protocol.rs:118-154, search.rs:671-751, histogram.rs:390-463,
@@ -596,6 +598,41 @@ int oracle_best_leader(void* h, const uint32_t* servers, uint32_t ns, const uint
   Bote b{(Planet*)h};
   std::vector<uint32_t> s(servers, servers + ns), c(clients, clients + nc);
   *out_pos = (uint32_t)b.best_leader(s, c, q, stat, nullptr);
+  ORACLE_CATCH
+}
+
+// Bote::leaderless (lib.rs:38-59) for a batch of configs (region ids, config
+// order) and nq quorum sizes: Input clients, then Colocated (the config).
+//   out_vals: ncfg x nq x (nc + n) u64
+int oracle_leaderless_batch(void* h, const uint32_t* configs, uint32_t ncfg, uint32_t n, const uint32_t* clients,
+                            uint32_t nc, const uint32_t* qs, uint32_t nq, uint32_t threads, uint64_t* out_vals) {
+  ORACLE_TRY
+  Bote b{(Planet*)h};
+  std::vector<uint32_t> cl(clients, clients + nc);
+  if (threads == 0) threads = 1;
+  std::vector<std::string> errs(threads);
+  auto work = [&](uint32_t t) {
+    try {
+      for (uint64_t i = (uint64_t)ncfg * t / threads; i < (uint64_t)ncfg * (t + 1) / threads; ++i) {
+        std::vector<uint32_t> cfg(configs + i * n, configs + (i + 1) * n);
+        for (uint32_t qi = 0; qi < nq; ++qi) {
+          uint64_t* o = out_vals + (i * nq + qi) * (nc + n);
+          auto a = b.leaderless(cfg, cl, qs[qi]);
+          auto c = b.leaderless(cfg, cfg, qs[qi]);
+          std::copy(a.begin(), a.end(), o);
+          std::copy(c.begin(), c.end(), o + nc);
+        }
+      }
+    } catch (const std::exception& ex) {
+      errs[t] = ex.what();
+    }
+  };
+  std::vector<std::thread> pool;
+  for (uint32_t t = 1; t < threads; ++t) pool.emplace_back(work, t);
+  work(0);
+  for (auto& th : pool) th.join();
+  for (auto& e : errs)
+    if (!e.empty()) throw Panic(e);
   ORACLE_CATCH
 }
 

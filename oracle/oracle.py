@@ -54,6 +54,8 @@ def lib():
                                     C.c_uint32, u64p]
         L.oracle_best_leader.argtypes = [C.c_void_p, u32p, C.c_uint32, u32p, C.c_uint32, C.c_uint32,
                                          C.c_int, C.POINTER(C.c_uint32)]
+        L.oracle_leaderless_batch.argtypes = [C.c_void_p, u32p, C.c_uint32, C.c_uint32, u32p, C.c_uint32, u32p,
+                                              C.c_uint32, C.c_uint32, u64p]
         L.oracle_hist_stats.argtypes = [u64p, C.c_uint32, f64p]
         L.oracle_hist_percentile.argtypes = [u64p, C.c_uint32, C.c_double, C.POINTER(C.c_double)]
         L.oracle_hist_fmt.argtypes = [u64p, C.c_uint32, C.c_char_p, C.c_uint32]
@@ -122,6 +124,17 @@ class OraclePlanet:
         s, c = _u32(servers), _u32(clients)
         out = np.zeros(len(c), np.uint64)
         _check(lib().oracle_leaderless(self.h, s, len(s), c, len(c), q, out))
+        return out
+
+    def leaderless_batch(self, configs: np.ndarray, clients, qs, threads: int = 1) -> np.ndarray:
+        """Bote::leaderless for each config (rows of region ids) and quorum size:
+        (ncfg, nq, nc + n) u64 — Input clients, then Colocated (config order)."""
+        cfg = _u32(configs)
+        ncfg, n = cfg.shape
+        c, q = _u32(clients), _u32(qs)
+        out = np.zeros((ncfg, len(q), len(c) + n), np.uint64)
+        _check(lib().oracle_leaderless_batch(self.h, cfg.reshape(-1), ncfg, n, c, len(c), q, len(q), threads,
+                                             out.reshape(-1)))
         return out
 
     def leader(self, leader: int, servers, clients, q: int) -> np.ndarray:

@@ -116,3 +116,57 @@ def test_per_call_entries_concurrent_handles():
     for t in th:
         t.join()
     assert not errors, errors
+
+
+def test_tempo_quorums_every_gcp_config():
+    """BASELINE config 2's Tempo keys on the whole GCP planet: for EVERY config
+    of every n = 3..13 and f = 1, 2, Tempo's fast (n/2+f), tiny fast (2f) and
+    write (f+1) quorums (fantoch/src/config.rs:317-329) through
+    bote_eval_leaderless equal the oracle's Bote::leaderless: exact sums and
+    sums of squares for every config (Input and Colocated), full per-client
+    vectors for a sample."""
+    from math import comb
+
+    from fantoch_amd.bote import eval_leaderless, tempo_quorums
+
+    p = Planet.new()
+    dp = DevicePlanet(p)
+    o = O.OraclePlanet.of(p)
+    srv = np.arange(p.R, dtype=np.uint32)
+    for n in range(3, 14):
+        qs = sorted({q for _, _, q in tempo_quorums(n)})
+        total = comb(p.R, n)
+        for rb in range(0, total, 40_000):
+            cnt = min(40_000, total - rb)
+            r = eval_leaderless(dp, srv, srv, n, qs, rank_begin=rb, ncfg=cnt, values=True)
+            cfg = np.array([_lib.colex_unrank(x, n, p.R) for x in range(rb, rb + cnt)], dtype=np.uint32)
+            ov = o.leaderless_batch(srv[cfg], srv, qs, threads=8)
+            nc = p.R
+            assert np.array_equal(r.s1[:, :, 0], ov[:, :, :nc].sum(axis=2)), n
+            assert np.array_equal(r.s1[:, :, 1], ov[:, :, nc:].sum(axis=2)), n
+            assert np.array_equal(r.s2[:, :, 0], (ov[:, :, :nc] ** 2).sum(axis=2)), n
+            assert np.array_equal(r.s2[:, :, 1], (ov[:, :, nc:] ** 2).sum(axis=2)), n
+            assert np.array_equal(r.vals[::97].astype(np.uint64), ov[::97]), n
+
+
+def test_tempo_stats_keys_and_unsorted_configs():
+    """Search.compute_stats(..., tempo=True) adds tf/ttf/twf keys whose
+    histograms equal the oracle's leaderless for an unsorted server list and
+    a client subset with repeats."""
+    from fantoch_amd.bote import Search, tempo_quorums
+    from fantoch_amd.protocol import ClientPlacement
+
+    p = Planet.new()
+    b = Bote(p)
+    o = O.OraclePlanet.of(p)
+    rng = np.random.default_rng(11)
+    for n in (3, 5, 7, 9, 13):
+        cfg = rng.choice(p.R, n, replace=False)
+        cli = rng.choice(p.R, 15, replace=True)
+        st = Search.compute_stats([p.names[i] for i in cfg], [p.names[i] for i in cli], b, tempo=True)
+        for proto, f, q in tempo_quorums(n):
+            want_i = sorted(o.leaderless(cfg, cli, q).tolist())
+            want_c = sorted(o.leaderless(cfg, cfg, q).tolist())
+            assert list(st.get(proto, f, ClientPlacement.Input).iter_values()) == want_i
+            assert list(st.get(proto, f, ClientPlacement.Colocated).iter_values()) == want_c
+        assert "af1" in st.map and "e" in st.map  # the reference's keys are still there

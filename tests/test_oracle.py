@@ -180,3 +180,34 @@ def test_colex_unrank_roundtrip():
         assert sum(comb(x, j + 1) for j, x in enumerate(c)) == r
         seen.add(tuple(c))
     assert len(seen) == comb(ns, n)
+
+
+def test_leaderless_batch_equals_single_calls():
+    """oracle_leaderless_batch (the Tempo parity checker) is Bote::leaderless
+    per config and quorum size (lib.rs:38-59)."""
+    from fantoch_amd.planet import Planet
+    p = Planet.new()
+    o = O.OraclePlanet.of(p)
+    rng = np.random.default_rng(3)
+    cfgs = np.array([rng.choice(p.R, 7, replace=False) for _ in range(20)], dtype=np.uint32)
+    cli = rng.choice(p.R, 9, replace=True)
+    qs = [2, 3, 4, 5]
+    got = o.leaderless_batch(cfgs, cli, qs, threads=2)
+    for i, cfg in enumerate(cfgs):
+        for qi, q in enumerate(qs):
+            assert got[i, qi, :9].tolist() == o.leaderless(cfg, cli, q).tolist()
+            assert got[i, qi, 9:].tolist() == o.leaderless(cfg, cfg, q).tolist()
+
+
+def test_tempo_quorum_sizes_known_answers():
+    """fantoch/src/config.rs:531-548 (tempo_parameters)."""
+    from fantoch_amd.protocol import Protocol, tempo_quorum_sizes
+    assert tempo_quorum_sizes(7, 1, False) == (4, 2, 4)
+    assert tempo_quorum_sizes(7, 2, False) == (5, 3, 4)
+    assert tempo_quorum_sizes(7, 1, True) == (2, 2, 6)
+    assert tempo_quorum_sizes(7, 2, True) == (4, 3, 5)
+    for n in range(3, 14):
+        for f in (1, 2):
+            assert Protocol.Tempo.quorum_size(n, f) == tempo_quorum_sizes(n, f, False)[0]
+            assert Protocol.TempoTiny.quorum_size(n, f) == tempo_quorum_sizes(n, f, True)[0]
+            assert Protocol.TempoWrite.quorum_size(n, f) == tempo_quorum_sizes(n, f, True)[1]
