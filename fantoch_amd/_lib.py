@@ -38,7 +38,7 @@ EXPORTS = [
     "bote_sweep_create", "bote_sweep_launch", "bote_sweep_result", "bote_sweep_result_bytes",
     "bote_sweep_result_device", "bote_merge_device", "bote_sweep_last_kernel_ms",
     "bote_sweep_destroy", "bote_colex_unrank", "bote_binomial", "bote_sweep_timing_reset",
-    "bote_sweep_timing", "bote_sweep_grid", "bote_sweep_is_fast", "bote_sweep_create_ex", "bote_search_topk", "bote_sweep_deferred", "bote_eval_leaderless",
+    "bote_sweep_timing", "bote_sweep_grid", "bote_sweep_is_fast", "bote_sweep_create_ex", "bote_search_topk", "bote_sweep_deferred", "bote_eval_leaderless", "bote_evolving_chains",
 ]
 KERNELS = {None: 0, "auto": 0, "generic": 1, "fast": 2, "group": 3}
 
@@ -111,6 +111,8 @@ def lib():
                             C.c_uint64, C.POINTER(RankingParamsC), _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]
     L.bote_eval_leaderless.argtypes = [_vp, _u32p, C.c_uint32, _u32p, C.c_uint32, C.c_uint32, _vp, C.c_uint64,
                                        C.c_uint64, _u32p, C.c_uint32, _vp, _vp, _vp]
+    L.bote_evolving_chains.argtypes = [C.c_int, C.c_uint32, _u32p, _vp, _vp, _vp, C.c_double, C.c_int, C.c_uint64,
+                                       _vp, _vp, C.POINTER(C.c_uint64)]
     L.bote_sweep_create.argtypes = [_vp, _u32p, C.c_uint32, _u32p, C.c_uint32, C.c_uint32,
                                     C.POINTER(Objective), C.c_uint32, C.c_uint32,
                                     C.POINTER(RankingParamsC), C.c_int, C.POINTER(_vp)]

@@ -509,47 +509,88 @@ class Search:
             ranked[n] = [(float(r.score[i]), int(i)) for i in idx]
         return ranked
 
-    def sorted_evolving_configs(self, p: RankingParams):
-        """search.rs:97-178: chains n = 3 -> 5 -> ... -> 13 of supersets, highest score first."""
+    def evolving_chain_arrays(self, p: RankingParams, limit: Optional[int] = None) -> List[dict]:
+        """The device chain search (bote_evolving_chains) per client set, as
+        arrays: {"ci", "total", "idx" (nout, 6) config indices per level (n = 3,
+        5, .., 13) into all_configs[ci][1][n]["cfg"], "score" (nout,)}, each
+        set's chains in the reference's order (score descending, equal scores
+        in enumeration order).  `limit` caps the chains fetched per set."""
         assert p.min_n == 3 and p.max_n == 13
-        results: Dict[F64, list] = {}
+        u64p = C.POINTER(C.c_uint64)
+        f64p = C.POINTER(C.c_double)
+        out = []
         for ci, (clients, configs) in enumerate(self.all_configs):
             ranked = self._rank(configs, p, ci)
-            masks = {n: {i: self._config_set(ci, n, i) for _, i in lst} for n, lst in ranked.items()}
-            means = {n: configs[n]["mean"] for n in ranked}
-
-            def supers(n, prev_n, prev_i):
-                prev = masks[prev_n][prev_i]
-                fs = p.ft_metric.fs(n - 2)
-                out = []
-                for score, i in ranked[n]:
-                    cs = masks[n][i]
-                    if cs.mask & prev.mask != prev.mask:
-                        continue
-                    ok = True
-                    for f in fs:  # min_mean_decrease (search.rs:403-419)
-                        slot = 0 if f == 1 else 2
-                        if not (means[prev_n][prev_i, slot] - means[n][i, slot] >= p.min_mean_decrease):
-                            ok = False
-                            break
-                    if ok:
-                        out.append((score, i))
-                return out
-
-            for s3, i3 in ranked.get(3, []):
-                for s5, i5 in supers(5, 3, i3):
-                    for s7, i7 in supers(7, 5, i5):
-                        for s9, i9 in supers(9, 7, i7):
-                            for s11, i11 in supers(11, 9, i9):
-                                for s13, i13 in supers(13, 11, i11):
-                                    score = s3 + s5 + s7 + s9 + s11 + s13
-                                    chain = [masks[3][i3], masks[5][i5], masks[7][i7], masks[9][i9],
-                                             masks[11][i11], masks[13][i13]]
-                                    results.setdefault(F64(score), []).append((F64(score), chain, clients))
-        out = []
-        for key in sorted(results.keys(), reverse=True):
-            out.extend(results[key])
+            counts = np.zeros(6, np.uint32)
+            keep, arrs = [], []
+            for lvl in range(6):
+                n = 3 + 2 * lvl
+                lst = ranked.get(n, [])
+                idx = np.array([i for _, i in lst], dtype=np.int64)
+                d = configs.get(n)
+                if len(idx) and len(d["srv"]) > 64:
+                    raise ValueError("chain search needs a server list of at most 64 regions")
+                pos = d["cfg"][idx].astype(np.uint64) if len(idx) else np.zeros((0, n), np.uint64)
+                mask = np.ascontiguousarray(np.bitwise_or.reduce(np.uint64(1) << pos, axis=1)
+                                            if len(idx) else np.zeros(0, np.uint64), dtype=np.uint64)
+                score = np.ascontiguousarray([sc for sc, _ in lst], dtype=np.float64)
+                mean = np.ascontiguousarray(d["mean"][idx][:, [0, 2]] if len(idx) else np.zeros((0, 2)),
+                                            dtype=np.float64)
+                counts[lvl] = len(idx)
+                keep.append(idx)
+                arrs.append((mask, score, mean))
+            ns = len(configs[3]["srv"]) if 3 in configs else 0
+            if counts.min() == 0 or ns == 0:
+                continue
+            masks = (u64p * 6)(*[x[0].ctypes.data_as(u64p) for x in arrs])
+            scores = (f64p * 6)(*[x[1].ctypes.data_as(f64p) for x in arrs])
+            means = (f64p * 6)(*[x[2].ctypes.data_as(f64p) for x in arrs])
+            total = C.c_uint64()
+            check(lib().bote_evolving_chains(self.dp.device, ns, counts, masks, scores, means,
+                                             float(p.min_mean_decrease), int(p.ft_metric.value), 0, None, None,
+                                             C.byref(total)))
+            nout = total.value if limit is None else min(limit, total.value)
+            out_idx = np.zeros((nout, 6), np.uint32)
+            out_sc = np.zeros(nout, np.float64)
+            if nout:
+                check(lib().bote_evolving_chains(self.dp.device, ns, counts, masks, scores, means,
+                                                 float(p.min_mean_decrease), int(p.ft_metric.value), nout,
+                                                 ptr(out_idx), ptr(out_sc), C.byref(total)))
+            idx = np.stack([keep[lvl][out_idx[:, lvl]] for lvl in range(6)], axis=1) if nout else \
+                np.zeros((0, 6), np.int64)
+            out.append({"ci": ci, "total": total.value, "idx": idx, "score": out_sc})
         return out
+
+    def chains_digest(self, arrays: dict) -> int:
+        """Order-dependent digest of one client set's chains (the oracle's
+        oracle_search_chains digest): h = bits(score); h = mix64(h ^ mask_l)
+        over the 6 configs' region-id bitmasks; sum over k of mix64(h + k)."""
+        ci = arrays["ci"]
+        configs = self.all_configs[ci][1]
+        h = np.ascontiguousarray(arrays["score"], dtype=np.float64).view(np.uint64).copy()
+        for lvl in range(6):
+            d = configs[3 + 2 * lvl]
+            regs = d["srv"][d["cfg"][arrays["idx"][:, lvl]]].astype(np.uint64)
+            m = np.bitwise_or.reduce(np.uint64(1) << regs, axis=1) if len(regs) else np.zeros(0, np.uint64)
+            h = _mix64(h ^ m)
+        k = np.arange(len(h), dtype=np.uint64)
+        return int(np.sum(_mix64(h + k), dtype=np.uint64))
+
+    def sorted_evolving_configs(self, p: RankingParams, limit: Optional[int] = None):
+        """search.rs:97-178: chains n = 3 -> 5 -> ... -> 13 of supersets, highest
+        score first (equal scores: client-set order, then enumeration order).
+        The superset/min_mean_decrease joins and the ordering run on the device
+        (bote_evolving_chains); `limit` caps the chains returned per client set."""
+        found = []  # (orderable key, client set, position, score, chain)
+        for a in self.evolving_chain_arrays(p, limit):
+            ci = a["ci"]
+            clients = self.all_configs[ci][0]
+            keys = ~(_orderable(a["score"]))
+            for k in range(len(a["score"])):
+                chain = [self._config_set(ci, 3 + 2 * lvl, int(a["idx"][k, lvl])) for lvl in range(6)]
+                found.append((int(keys[k]), ci, k, F64(float(a["score"][k])), chain, clients))
+        found.sort(key=lambda x: (x[0], x[1], x[2]))
+        return [(sc, chain, clients) for _, _, _, sc, chain, clients in found]
 
     @staticmethod
     def stats_fmt(stats: ProtocolStats, n: int) -> str:
@@ -561,6 +602,22 @@ class Search:
                 fmt += f"{stats.fmt(Protocol.Atlas, f, placement)} {stats.fmt(Protocol.FPaxos, f, placement)} "
             out += f"{fmt}{stats.fmt(Protocol.EPaxos, 0, placement)} "
         return out
+
+
+def _mix64(z: np.ndarray) -> np.ndarray:
+    """splitmix64 finaliser on uint64 arrays (wrapping)."""
+    z = z + np.uint64(0x9E3779B97F4A7C15)
+    z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+    z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    return z ^ (z >> np.uint64(31))
+
+
+def _orderable(x: np.ndarray) -> np.ndarray:
+    """F64 total order as uint64 keys (NaN greatest; -0.0 == 0.0)."""
+    x = np.asarray(x, dtype=np.float64) + 0.0
+    x = np.where(np.isnan(x), np.float64("nan"), x)
+    b = x.view(np.uint64)
+    return np.where(b >> np.uint64(63), ~b, b | np.uint64(0x8000000000000000))
 
 
 def compute_score_host(n: int, stats: ProtocolStats, p: RankingParams) -> Tuple[bool, F64]:

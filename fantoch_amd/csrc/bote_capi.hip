@@ -599,6 +599,40 @@ int bote_eval_leaderless(const bote_planet* p, const uint32_t* servers, uint32_t
   return BOTE_OK;
 }
 
+// ---------------------------------------- superset chains (ranking product)
+int bote_evolving_chains(int device, uint32_t ns, const uint32_t* counts, const uint64_t* const* masks,
+                         const double* const* scores, const double* const* means, double min_mean_decrease,
+                         int ft_metric, uint64_t max_out, uint32_t* out_idx, double* out_score, uint64_t* out_total) {
+  if (!counts || !masks || !scores || !means || !out_total) return fail(BOTE_E_ARG, "null argument");
+  if (ns == 0 || ns > 64) return fail(BOTE_E_RANGE, "the server list must hold 1 to 64 regions");
+  if (ft_metric != BOTE_FT_F1 && ft_metric != BOTE_FT_F1F2) return fail(BOTE_E_ARG, "bad ft_metric");
+  if (max_out && (!out_idx || !out_score)) return fail(BOTE_E_ARG, "null output");
+  bote::ChainHostLevel lv[6];
+  for (int l = 0; l < 6; ++l) {
+    const uint32_t n = 3 + 2 * l;
+    if (counts[l] && (!masks[l] || !scores[l] || !means[l])) return fail(BOTE_E_ARG, "null level array");
+    for (uint32_t i = 0; i < counts[l]; ++i) {
+      const uint64_t m = masks[l][i];
+      if ((uint32_t)__builtin_popcountll(m) != n || (ns < 64 && (m >> ns)))
+        return fail(BOTE_E_ARG, "level mask is not an n-subset of the server list");
+    }
+    lv[l] = bote::ChainHostLevel{counts[l], n, masks[l], scores[l], means[l]};
+  }
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(BOTE_E_NODEV, "no HIP device");
+  if (device < 0 || device >= ndev) return fail(BOTE_E_ARG, "device out of range");
+  HIP_TRY(hipSetDevice(device));
+  hipStream_t st = nullptr;
+  HIP_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  int too_many = 0;
+  hipError_t e = bote::chain_search(lv, ns, ft_metric, min_mean_decrease, max_out, out_idx, out_score, out_total, st,
+                                    &too_many);
+  (void)hipStreamDestroy(st);
+  if (e != hipSuccess) return fail(BOTE_E_DEVICE, std::string("chain search: ") + hipGetErrorString(e));
+  if (too_many) return fail(BOTE_E_RANGE, "more than 2^31 chain prefixes at one level");
+  return BOTE_OK;
+}
+
 // ------------------------------------------------------------------ sweep
 int bote_sweep_create(const bote_planet* p, const uint32_t* servers, uint32_t ns, const uint32_t* clients,
                       uint32_t nc, uint32_t n, const bote_objective* objs, uint32_t n_obj, uint32_t K,

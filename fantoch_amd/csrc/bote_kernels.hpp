@@ -165,6 +165,16 @@ struct LqArgs {
 size_t lq_smem_bytes(const LqArgs& a, uint32_t n);
 hipError_t launch_leaderless_q(const LqArgs& a, uint32_t n, uint32_t grid, size_t shm, hipStream_t st);
 
+// ---- Search::sorted_evolving_configs on the device (bote_chain.hip)
+struct ChainHostLevel {
+  uint32_t cnt, n;
+  const uint64_t* mask;
+  const double* score;
+  const double* mean;
+};
+hipError_t chain_search(const ChainHostLevel* lv, uint32_t ns, int ft_metric, double min_dec, uint64_t max_out,
+                        uint32_t* out_idx, double* out_score, uint64_t* out_total, hipStream_t st, int* too_many);
+
 hipError_t launch_single(const SingleArgs& a, int mode, hipStream_t st);
 hipError_t launch_best_leader(const SingleArgs& a, const uint64_t* vals, double* stat, hipStream_t st);
 

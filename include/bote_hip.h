@@ -187,6 +187,23 @@ int bote_eval_leaderless(const bote_planet* p, const uint32_t* servers, uint32_t
                          uint64_t rank_begin, uint64_t ncfg, const uint32_t* quorum_sizes, uint32_t nq,
                          uint32_t* out_vals, uint64_t* out_sum, uint64_t* out_sumsq);
 
+/* -------------------------------------- superset chains (ranking product) --- */
+/* Search::sorted_evolving_configs (search.rs:97-178; super_configs :378-401,
+ * min_mean_decrease :403-419) for ONE client set, on `device`.  Level l = 0..5
+ * holds the ranked (valid) configs of n = 3 + 2l in enumeration order:
+ *   masks[l][i]    bitmask of the config's positions in the server list (ns <= 64)
+ *   scores[l][i]   Search::compute_score
+ *   means[l][2i], means[l][2i+1]  Histogram::mean of the Atlas Input key, f = 1, 2
+ * A chain takes one config per level, each a superset of the previous whose
+ * Atlas means decrease by >= min_mean_decrease for f in FTMetric::fs(n - 2).
+ * Out: *out_total chains; the first max_out in the reference's order (score
+ * descending, equal scores in enumeration order): out_idx (6 level indices
+ * per chain) and out_score (s3 + s5 + ... + s13, summed in that order). */
+int bote_evolving_chains(int device, uint32_t ns, const uint32_t* counts, const uint64_t* const* masks,
+                         const double* const* scores, const double* const* means,
+                         double min_mean_decrease, int ft_metric, uint64_t max_out,
+                         uint32_t* out_idx, double* out_score, uint64_t* out_total);
+
 /* ------------------------------------------------ streaming search (hot) --- */
 /* The exhaustive sweep (search.rs:199-260 + compute_stats + compute_score)
  * over colex ranks [rank_begin, rank_end) of n-subsets of `servers`, keeping

@@ -8,7 +8,7 @@ fn main() {
         return;
     }
     let status = Command::new("make")
-        .args(["-C", &format!("{}/fantoch_amd/csrc", hip), "ARCH=gfx950"])
+        .args(&["-C", &format!("{}/fantoch_amd/csrc", hip), "ARCH=gfx950"])
         .status()
         .expect("make libbote_hip.so");
     assert!(status.success(), "libbote_hip.so build failed");

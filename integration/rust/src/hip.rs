@@ -17,6 +17,14 @@ pub const BOTE_ATLAS: c_int = 2;
 pub const BOTE_TEMPO: c_int = 3;
 pub const BOTE_TEMPO_TINY: c_int = 4;
 
+pub const BOTE_KERNEL_AUTO: c_int = 0;
+pub const BOTE_KERNEL_GENERIC: c_int = 1;
+pub const BOTE_KERNEL_FAST: c_int = 2;
+pub const BOTE_KERNEL_GROUP: c_int = 3;
+
+pub const BOTE_FT_F1: i32 = 1;
+pub const BOTE_FT_F1F2: i32 = 2;
+
 pub const BOTE_STAT_MEAN: c_int = 0;
 pub const BOTE_STAT_COV: c_int = 1;
 pub const BOTE_STAT_MDTM: c_int = 2;
@@ -80,13 +88,36 @@ extern "C" {
     pub fn bote_sweep_create(p: *const bote_planet, servers: *const u32, ns: u32, clients: *const u32, nc: u32,
                              n: u32, objs: *const bote_objective, n_obj: u32, k: u32,
                              rp: *const bote_ranking_params, digest: c_int, out: *mut *mut bote_sweep) -> c_int;
+    pub fn bote_sweep_create_ex(p: *const bote_planet, servers: *const u32, ns: u32, clients: *const u32, nc: u32,
+                                n: u32, objs: *const bote_objective, n_obj: u32, k: u32,
+                                rp: *const bote_ranking_params, digest: c_int, kernel: c_int,
+                                out: *mut *mut bote_sweep) -> c_int;
     pub fn bote_sweep_launch(s: *mut bote_sweep, rank_begin: u64, rank_end: u64, stream: *mut c_void) -> c_int;
+    pub fn bote_sweep_deferred(s: *mut bote_sweep, stream: *mut c_void, out: *mut u64) -> c_int;
+    pub fn bote_eval_leaderless(p: *const bote_planet, servers: *const u32, ns: u32, clients: *const u32, nc: u32,
+                                n: u32, configs: *const u32, rank_begin: u64, ncfg: u64, quorum_sizes: *const u32,
+                                nq: u32, out_vals: *mut u32, out_sum: *mut u64, out_sumsq: *mut u64) -> c_int;
+    pub fn bote_search_topk(planets: *const *const bote_planet, n_devices: u32, servers: *const u32, ns: u32,
+                            clients: *const u32, nc: u32, n: u32, rank_begin: u64, rank_end: u64,
+                            objs: *const bote_objective, n_obj: u32, k: u32, rp: *const bote_ranking_params,
+                            digest: c_int, out: *mut bote_topk_record, out_count: *mut u32, out_valid: *mut u64,
+                            out_digest: *mut u64) -> c_int;
+    pub fn bote_evolving_chains(device: c_int, ns: u32, counts: *const u32, masks: *const *const u64,
+                                scores: *const *const f64, means: *const *const f64, min_mean_decrease: f64,
+                                ft_metric: c_int, max_out: u64, out_idx: *mut u32, out_score: *mut f64,
+                                out_total: *mut u64) -> c_int;
     pub fn bote_sweep_result(s: *mut bote_sweep, stream: *mut c_void, out: *mut bote_topk_record,
                              out_count: *mut u32, out_valid: *mut u64, out_digest: *mut u64) -> c_int;
     pub fn bote_sweep_result_bytes(s: *const bote_sweep) -> u64;
     pub fn bote_sweep_result_device(s: *mut bote_sweep, dst: *mut c_void, stream: *mut c_void) -> c_int;
     pub fn bote_merge_device(s: *const bote_sweep, src: *const c_void, n_shards: u32, dst: *mut c_void,
                              stream: *mut c_void) -> c_int;
+    pub fn bote_sweep_last_kernel_ms(s: *mut bote_sweep, out_ms: *mut f32) -> c_int;
+    pub fn bote_sweep_timing_reset(s: *mut bote_sweep) -> c_int;
+    pub fn bote_sweep_timing(s: *mut bote_sweep, out_total_ms: *mut f32, out_launches: *mut u32) -> c_int;
+    pub fn bote_sweep_is_fast(s: *const bote_sweep, out: *mut c_int) -> c_int;
+    pub fn bote_sweep_grid(s: *const bote_sweep, out_grid: *mut u32, out_block: *mut u32, out_lds_bytes: *mut u32)
+        -> c_int;
     pub fn bote_sweep_destroy(s: *mut bote_sweep) -> c_int;
     pub fn bote_colex_unrank(rank: u64, n: u32, ns: u32, out_positions: *mut u32) -> c_int;
     pub fn bote_binomial(ns: u32, n: u32) -> u64;

@@ -1,6 +1,11 @@
 //! `Bote` / `Search` entry points over libbote_hip.so, keeping the reference
 //! signatures (fantoch_bote/src/lib.rs:38-121, search.rs:262-319).  Sketch for
 //! maintainers; not compiled here (no cargo in the image).
+//! Written against the reference's real types: `Protocol` is neither `Copy`
+//! nor `PartialEq` (fantoch_bote/src/protocol.rs:5-9), `ProtocolStats::insert`
+//! takes (protocol, f, placement, stats) (protocol.rs:76-82), `Planet::regions`
+//! returns an owned `Vec<Region>` (fantoch/src/planet/mod.rs:102), and the
+//! crate is edition 2018 (no by-value array iteration).
 use crate::hip;
 use fantoch::metrics::Histogram;
 use fantoch::planet::{Planet, Region};
@@ -16,7 +21,7 @@ pub struct HipBote {
 
 impl HipBote {
     pub fn from(planet: &Planet, device: i32) -> Self {
-        let mut names: Vec<Region> = planet.regions().into_iter().cloned().collect();
+        let mut names: Vec<Region> = planet.regions();
         names.sort();
         let r = names.len();
         let mut lat = vec![0u16; r * r];
@@ -78,20 +83,52 @@ impl HipBote {
         // slot layout (include/bote_hip.h, bote_eval): af1 ff1 af2 ff2 e for
         // Input (nc values each), then the same five for Colocated (n values)
         let max_f = std::cmp::min(n / 2, 2);
-        let keys = [(Protocol::Atlas, 1), (Protocol::FPaxos, 1), (Protocol::Atlas, 2), (Protocol::FPaxos, 2),
-                    (Protocol::EPaxos, 0)];
+        // slot k -> (protocol, f); Protocol is not Copy, so it is built per use
+        fn slot_protocol(k: usize) -> Protocol {
+            match k {
+                0 | 2 => Protocol::Atlas,
+                1 | 3 => Protocol::FPaxos,
+                _ => Protocol::EPaxos,
+            }
+        }
+        const SLOT_F: [usize; 5] = [1, 1, 2, 2, 0];
         let mut stats = ProtocolStats::new();
-        for (placement, base, len) in [(ClientPlacement::Input, 0, nc), (ClientPlacement::Colocated, 5 * nc, n)] {
-            for (k, (proto, f)) in keys.iter().enumerate() {
-                if *proto != Protocol::EPaxos && *f > max_f {
+        let placements = [(ClientPlacement::Input, 0, nc), (ClientPlacement::Colocated, 5 * nc, n)];
+        for &(placement, base, len) in placements.iter() {
+            for k in 0..5 {
+                let f = SLOT_F[k];
+                if k != 4 && f > max_f {
                     continue;
                 }
                 let v = &vals[base + k * len..base + (k + 1) * len];
                 let hist = Histogram::from(v.iter().map(|x| *x as u64));
-                stats.insert(*proto, placement, *f, hist);
+                stats.insert(slot_protocol(k), f, placement, hist);
             }
         }
         stats
+    }
+
+    /// The multi-GPU exhaustive search in one call (bote_search_topk): colex
+    /// ranks of n-subsets of `servers` sharded over `others` and this planet,
+    /// merged on this planet's device; records ascending by (key, rank).
+    pub fn search_topk(&self, others: &[&HipBote], servers: &[Region], clients: &[Region], n: usize,
+                       objectives: &[hip::bote_objective], k: usize, rp: &hip::bote_ranking_params)
+        -> (Vec<Vec<hip::bote_topk_record>>, u64, u64) {
+        let (s, c) = (self.ids(servers), self.ids(clients));
+        let mut planets: Vec<*const hip::bote_planet> = vec![self.dev as *const _];
+        planets.extend(others.iter().map(|b| b.dev as *const _));
+        let total = unsafe { hip::bote_binomial(s.len() as u32, n as u32) };
+        let no = objectives.len();
+        let mut recs = vec![hip::bote_topk_record { key: 0, rank: 0 }; no * k];
+        let mut cnt = vec![0u32; no];
+        let (mut valid, mut digest) = (0u64, 0u64);
+        hip::check(unsafe {
+            hip::bote_search_topk(planets.as_ptr(), planets.len() as u32, s.as_ptr(), s.len() as u32, c.as_ptr(),
+                                  c.len() as u32, n as u32, 0, total, objectives.as_ptr(), no as u32, k as u32, rp,
+                                  1, recs.as_mut_ptr(), cnt.as_mut_ptr(), &mut valid, &mut digest)
+        });
+        let tops = (0..no).map(|o| recs[o * k..o * k + cnt[o] as usize].to_vec()).collect();
+        (tops, valid, digest)
     }
 }
 

@@ -798,94 +798,97 @@ int oracle_sweep(void* h, const uint32_t* servers, uint32_t ns, const uint32_t* 
 // Search::new + sorted_evolving_configs (search.rs:47-178) for a single client
 // set (R13C13 / R17C17 / R20C20), configs enumerated in lexicographic order of
 // positions in `servers` (permutator order is not pinned).
-//   out_score:   best chain's score (F64)
-//   out_chain:   6 configs (n = 3,5,..,13) as region ids, ascending by name
-//                (BTreeSet<Region> order), each padded to 13 entries
-//   out_fmt:     6 stats_fmt strings, '\n'-separated
-//   out_nchains: number of chains found
+// Chains in the reference's order: score descending (BTreeMap<F64, Vec<_>>
+// iterated in reverse), equal scores in nested-loop insertion order.
+struct ChainSearch {
+  struct CS {
+    std::vector<uint32_t> set;  // sorted by name
+    std::vector<bool> mask;
+    ProtocolStats st;
+  };
+  struct F64Less {
+    bool operator()(double a, double b) const { return f64_cmp(a, b) < 0; }
+  };
+  std::map<size_t, std::vector<CS>> configs;
+  std::map<double, std::vector<std::vector<const CS*>>, F64Less> chains;
+  uint64_t nchains = 0;
+
+  ChainSearch(const Planet* P, const uint32_t* servers, uint32_t ns, const uint32_t* clients, uint32_t nc,
+              const RankingParams& rp) {
+    Bote b{P};
+    std::vector<uint32_t> cl(clients, clients + nc);
+    for (size_t n = 3; n <= 13; n += 2) {
+      auto& vec = configs[n];
+      if (n > ns) continue;
+      std::vector<uint32_t> idx(n);
+      for (size_t j = 0; j < n; ++j) idx[j] = (uint32_t)j;
+      for (;;) {
+        CS cs;
+        std::vector<uint32_t> cfg(n);
+        for (size_t j = 0; j < n; ++j) cfg[j] = servers[idx[j]];
+        compute_stats(b, cfg, cl, cs.st);
+        cs.set = cfg;
+        std::sort(cs.set.begin(), cs.set.end(),
+                  [&](uint32_t a, uint32_t c) { return P->names[a] < P->names[c]; });
+        cs.mask.assign(P->R, false);
+        for (auto r : cfg) cs.mask[r] = true;
+        vec.push_back(std::move(cs));
+        // lexicographic successor
+        int j = (int)n - 1;
+        while (j >= 0 && idx[j] == ns - n + j) --j;
+        if (j < 0) break;
+        ++idx[j];
+        for (size_t k = j + 1; k < n; ++k) idx[k] = idx[k - 1] + 1;
+      }
+    }
+    // rank (search.rs:329-354)
+    std::map<size_t, std::vector<std::pair<double, const CS*>>> ranked;
+    for (auto& kv : configs) {
+      auto& out = ranked[kv.first];
+      for (auto& cs : kv.second) {
+        double score;
+        if (compute_score(kv.first, cs.st, rp, score)) out.emplace_back(score, &cs);
+      }
+    }
+    auto superset = [&](const CS& big, const CS& small) {
+      for (auto r : small.set)
+        if (!big.mask[r]) return false;
+      return true;
+    };
+    auto supers = [&](size_t n, const CS& prev) {
+      std::vector<std::pair<double, const CS*>> v;
+      for (auto& e : ranked[n])
+        if (superset(*e.second, prev) && min_mean_decrease(e.second->st, prev.st, n, rp)) v.push_back(e);
+      return v;
+    };
+    for (auto& e3 : ranked[3])
+      for (auto& e5 : supers(5, *e3.second))
+        for (auto& e7 : supers(7, *e5.second))
+          for (auto& e9 : supers(9, *e7.second))
+            for (auto& e11 : supers(11, *e9.second))
+              for (auto& e13 : supers(13, *e11.second)) {
+                double sc = e3.first + e5.first;
+                sc = sc + e7.first;
+                sc = sc + e9.first;
+                sc = sc + e11.first;
+                sc = sc + e13.first;
+                chains[sc].push_back({e3.second, e5.second, e7.second, e9.second, e11.second, e13.second});
+                ++nchains;
+              }
+  }
+};
+
 int oracle_search_best(void* h, const uint32_t* servers, uint32_t ns, const uint32_t* clients,
                        uint32_t nc, const double* rparams, int ft_metric, double* out_score,
                        uint32_t* out_chain, char* out_fmt, uint32_t fmt_cap,
                        uint64_t* out_nchains) {
   ORACLE_TRY
   const Planet* P = (Planet*)h;
-  Bote b{P};
-  std::vector<uint32_t> cl(clients, clients + nc);
   RankingParams rp{rparams[0], rparams[1], rparams[2], rparams[3], 3, 13, ft_metric};
-  struct CS {
-    std::vector<uint32_t> set;  // sorted by name
-    std::vector<bool> mask;
-    ProtocolStats st;
-  };
-  std::map<size_t, std::vector<CS>> configs;
-  for (size_t n = 3; n <= 13; n += 2) {
-    auto& vec = configs[n];
-    if (n > ns) continue;
-    std::vector<uint32_t> idx(n);
-    for (size_t j = 0; j < n; ++j) idx[j] = (uint32_t)j;
-    for (;;) {
-      CS cs;
-      std::vector<uint32_t> cfg(n);
-      for (size_t j = 0; j < n; ++j) cfg[j] = servers[idx[j]];
-      compute_stats(b, cfg, cl, cs.st);
-      cs.set = cfg;
-      std::sort(cs.set.begin(), cs.set.end(),
-                [&](uint32_t a, uint32_t c) { return P->names[a] < P->names[c]; });
-      cs.mask.assign(P->R, false);
-      for (auto r : cfg) cs.mask[r] = true;
-      vec.push_back(std::move(cs));
-      // lexicographic successor
-      int j = (int)n - 1;
-      while (j >= 0 && idx[j] == ns - n + j) --j;
-      if (j < 0) break;
-      ++idx[j];
-      for (size_t k = j + 1; k < n; ++k) idx[k] = idx[k - 1] + 1;
-    }
-  }
-  // rank (search.rs:329-354)
-  std::map<size_t, std::vector<std::pair<double, const CS*>>> ranked;
-  for (auto& kv : configs) {
-    auto& out = ranked[kv.first];
-    for (auto& cs : kv.second) {
-      double score;
-      if (compute_score(kv.first, cs.st, rp, score)) out.emplace_back(score, &cs);
-    }
-  }
-  auto superset = [&](const CS& big, const CS& small) {
-    for (auto r : small.set)
-      if (!big.mask[r]) return false;
-    return true;
-  };
-  auto supers = [&](size_t n, const CS& prev) {
-    std::vector<std::pair<double, const CS*>> v;
-    for (auto& e : ranked[n])
-      if (superset(*e.second, prev) && min_mean_decrease(e.second->st, prev.st, n, rp))
-        v.push_back(e);
-    return v;
-  };
-  struct F64Less {
-    bool operator()(double a, double b) const { return f64_cmp(a, b) < 0; }
-  };
-  std::map<double, std::vector<std::vector<const CS*>>, F64Less> chains;
-  uint64_t nchains = 0;
-  for (auto& e3 : ranked[3])
-    for (auto& e5 : supers(5, *e3.second))
-      for (auto& e7 : supers(7, *e5.second))
-        for (auto& e9 : supers(9, *e7.second))
-          for (auto& e11 : supers(11, *e9.second))
-            for (auto& e13 : supers(13, *e11.second)) {
-              double s = e3.first + e5.first;
-              s = s + e7.first;
-              s = s + e9.first;
-              s = s + e11.first;
-              s = s + e13.first;
-              chains[s].push_back({e3.second, e5.second, e7.second, e9.second, e11.second,
-                                   e13.second});
-              ++nchains;
-            }
-  *out_nchains = nchains;
-  if (chains.empty()) throw Panic("no chain");
-  auto& best = *chains.rbegin();
+  ChainSearch cs(P, servers, ns, clients, nc, rp);
+  *out_nchains = cs.nchains;
+  if (cs.chains.empty()) throw Panic("no chain");
+  auto& best = *cs.chains.rbegin();
   *out_score = best.first;
   const auto& css = best.second.front();
   std::string fmt;
@@ -908,6 +911,44 @@ int oracle_search_best(void* h, const uint32_t* servers, uint32_t ns, const uint
   }
   if (fmt.size() + 1 > fmt_cap) throw Panic("fmt buffer too small");
   memcpy(out_fmt, fmt.c_str(), fmt.size() + 1);
+  ORACLE_CATCH
+}
+
+// The first K chains of sorted_evolving_configs in the reference's order:
+//   out_score[k], out_chain[k][6][13] (region ids by name, ~0 padded); out_nchains = all chains.
+//   out_digest: order-dependent digest of ALL chains (tests/test_gpu_chains.py):
+//     h_k = bits(score_k); h_k = mix64(h_k ^ mask_l) for l = 0..5 (region-id bitmask, R <= 64);
+//     digest = sum_k mix64(h_k + k) mod 2^64
+int oracle_search_chains(void* h, const uint32_t* servers, uint32_t ns, const uint32_t* clients, uint32_t nc,
+                         const double* rparams, int ft_metric, uint32_t K, double* out_score, uint32_t* out_chain,
+                         uint64_t* out_nchains, uint64_t* out_digest) {
+  ORACLE_TRY
+  const Planet* P = (Planet*)h;
+  if (P->R > 64) throw Panic("chain digest needs R <= 64");
+  RankingParams rp{rparams[0], rparams[1], rparams[2], rparams[3], 3, 13, ft_metric};
+  ChainSearch cs(P, servers, ns, clients, nc, rp);
+  *out_nchains = cs.nchains;
+  uint64_t k = 0, dig = 0;
+  for (auto it = cs.chains.rbegin(); it != cs.chains.rend(); ++it)
+    for (auto& ch : it->second) {
+      if (k < K) {
+        out_score[k] = it->first;
+        for (size_t i = 0; i < 6; ++i)
+          for (size_t j = 0; j < 13; ++j)
+            out_chain[((size_t)k * 6 + i) * 13 + j] = j < ch[i]->set.size() ? ch[i]->set[j] : ~0u;
+      }
+      double sc = it->first;
+      uint64_t hk;
+      memcpy(&hk, &sc, 8);
+      for (size_t i = 0; i < 6; ++i) {
+        uint64_t m = 0;
+        for (auto r : ch[i]->set) m |= 1ull << r;
+        hk = mix64(hk ^ m);
+      }
+      dig += mix64(hk + k);
+      ++k;
+    }
+  *out_digest = dig;
   ORACLE_CATCH
 }
 

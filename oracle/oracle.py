@@ -75,6 +75,8 @@ def lib():
         L.oracle_search_best.argtypes = [C.c_void_p, u32p, C.c_uint32, u32p, C.c_uint32, f64p, C.c_int,
                                          C.POINTER(C.c_double), u32p, C.c_char_p, C.c_uint32,
                                          C.POINTER(C.c_uint64)]
+        L.oracle_search_chains.argtypes = [C.c_void_p, u32p, C.c_uint32, u32p, C.c_uint32, f64p, C.c_int, C.c_uint32,
+                                           f64p, u32p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
         _LIB = L
     return _LIB
 
@@ -199,6 +201,24 @@ class OraclePlanet:
                                         C.byref(score), chain, buf, len(buf), C.byref(nch)))
         sets = [[int(x) for x in chain[i * 13:(i + 1) * 13] if x != 0xFFFFFFFF] for i in range(6)]
         return score.value, sets, buf.value.decode().split("\n")[:6], nch.value
+
+
+    def search_chains(self, servers, clients, rparams=(110.0, 35.0, 0.0, 15.0), ft_metric: int = 2, K: int = 50):
+        """The first K chains of sorted_evolving_configs (reference order), the total count
+        and the order-dependent digest of all chains: ([(score, [[region ids by name] x 6])],
+        nchains, digest)."""
+        s, c = _u32(servers), _u32(clients)
+        sc = np.zeros(max(K, 1), np.float64)
+        ch = np.zeros(max(K, 1) * 6 * 13, np.uint32)
+        nch, dig = C.c_uint64(), C.c_uint64()
+        rp = np.asarray(rparams, dtype=np.float64)
+        _check(lib().oracle_search_chains(self.h, s, len(s), c, len(c), rp, ft_metric, K, sc, ch, C.byref(nch),
+                                          C.byref(dig)))
+        out = []
+        for k in range(min(K, nch.value)):
+            sets = [[int(x) for x in ch[(k * 6 + i) * 13:(k * 6 + i + 1) * 13] if x != 0xFFFFFFFF] for i in range(6)]
+            out.append((float(sc[k]), sets))
+        return out, nch.value, dig.value
 
 
 def hist_stats(values) -> np.ndarray:

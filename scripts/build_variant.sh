@@ -8,7 +8,7 @@ D=fantoch_amd/lib_$NAME
 mkdir -p $D/obj
 H="/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -Wno-unused-result $FLAGS"
 # GROUP_SRC: an alternative bote_group.hip (e.g. `git show HEAD:...` for an A/B of the committed kernel)
-for f in bote_kernels bote_sweep bote_group bote_quorums bote_capi; do
+for f in bote_kernels bote_sweep bote_group bote_quorums bote_chain bote_capi; do
   src=fantoch_amd/csrc/$f.hip
   if [ "$f" = bote_group ] && [ -n "${GROUP_SRC:-}" ]; then src=$GROUP_SRC; fi
   if [ "$f" = bote_group ] || [ ! -f $D/obj/$f.o ]; then $H -I fantoch_amd/csrc -c $src -o $D/obj/$f.o & fi

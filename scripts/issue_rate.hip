@@ -1,7 +1,8 @@
-// Front-end (instruction issue) probe for gfx950: the same integer add in
-// different encodings, and at different waves per SIMD.  If the VOP3 (8-byte)
-// and literal (8-byte) forms run at half the rate of the 4-byte VOP2 form, the
-// limit is instruction bytes, not VALU lanes.
+// VALU issue-rate probe for gfx950: chip-wide throughput of
+// each instruction the sweep kernels are built from, 8 waves per SIMD, 8
+// independent chains per lane.  Result (profiles/r02_issue_rate*.json): the
+// encoding size does not matter (v_add_u32 e32 = e64 = with a literal), but
+// packed (VOP3P), 3-source and multiply ops issue at ~58 % of the simple ops.
 //   hipcc --offload-arch=gfx950 -O3 scripts/issue_rate.hip -o /tmp/issue_rate && /tmp/issue_rate
 #include <hip/hip_runtime.h>
 #include <cstdio>
@@ -30,6 +31,29 @@ KERNEL(k_pk_add, "v_pk_add_u16 %0, %0, %1")            // 8 B (VOP3P)
 KERNEL(k_or_e32, "v_or_b32_e32 %0, %0, %1")            // 4 B
 KERNEL(k_lshl_add, "v_lshl_add_u32 %0, %0, 3, %1")     // 8 B
 KERNEL(k_add3, "v_add3_u32 %0, %0, %1, %1")            // 8 B, 2 adds
+KERNEL(k_min_u32, "v_min_u32_e32 %0, %0, %1")
+KERNEL(k_max_u32, "v_max_u32_e32 %0, %0, %1")
+KERNEL(k_lshl, "v_lshlrev_b32_e32 %0, 3, %0")
+KERNEL(k_lshr, "v_lshrrev_b32_e32 %0, %1, %0")
+KERNEL(k_bfe, "v_bfe_u32 %0, %0, 16, 4")
+KERNEL(k_and, "v_and_b32_e32 %0, %0, %1")
+KERNEL(k_xor, "v_xor_b32_e32 %0, %0, %1")
+KERNEL(k_perm, "v_perm_b32 %0, %0, %1, %1")
+KERNEL(k_pk_min, "v_pk_min_u16 %0, %0, %1")
+KERNEL(k_pk_lshr, "v_pk_lshrrev_b16 %0, 4, %0")
+KERNEL(k_dot2, "v_dot2_u32_u16 %0, %1, %1, %0")
+KERNEL(k_mul24, "v_mul_u32_u24_e32 %0, %0, %1")
+KERNEL(k_mad24, "v_mad_u32_u24 %0, %0, %1, %1")
+KERNEL(k_min3, "v_min3_u32 %0, %0, %1, %1")
+KERNEL(k_and_or, "v_and_or_b32 %0, %0, %1, %1")
+KERNEL(k_lshl_or, "v_lshl_or_b32 %0, %0, 3, %1")
+KERNEL(k_alignbit, "v_alignbit_b32 %0, %0, %1, 7")
+KERNEL(k_mul_lo, "v_mul_lo_u32 %0, %0, %1")
+KERNEL(k_cvt_f32, "v_cvt_f32_u32_e32 %0, %0")
+KERNEL(k_mul_f32, "v_mul_f32_e32 %0, %0, %1")
+KERNEL(k_fma_f32, "v_fma_f32 %0, %0, %1, %1")
+KERNEL(k_rcp_f32, "v_rcp_f32_e32 %0, %0")
+KERNEL(k_cndmask, "v_cndmask_b32_e32 %0, %0, %1, vcc")
 
 typedef void (*kfn)(unsigned*, unsigned, unsigned);
 
@@ -37,7 +61,15 @@ int main() {
   struct { const char* name; kfn f; int bytes; } ks[] = {
       {"v_add_u32_e32", k_add_e32, 4}, {"v_add_u32_e64", k_add_e64, 8}, {"v_add_u32_e32+literal", k_add_lit, 8},
       {"v_pk_add_u16", k_pk_add, 8},   {"v_or_b32_e32", k_or_e32, 4},   {"v_lshl_add_u32", k_lshl_add, 8},
-      {"v_add3_u32", k_add3, 8}};
+      {"v_add3_u32", k_add3, 8},       {"v_min_u32", k_min_u32, 4},     {"v_max_u32", k_max_u32, 4},
+      {"v_lshlrev_b32", k_lshl, 4},    {"v_lshrrev_b32", k_lshr, 4},    {"v_bfe_u32", k_bfe, 8},
+      {"v_and_b32", k_and, 4},         {"v_xor_b32", k_xor, 4},         {"v_perm_b32", k_perm, 8},
+      {"v_pk_min_u16", k_pk_min, 8},   {"v_pk_lshrrev_b16", k_pk_lshr, 8}, {"v_dot2_u32_u16", k_dot2, 8},
+      {"v_mul_u32_u24", k_mul24, 4},   {"v_mad_u32_u24", k_mad24, 8},   {"v_min3_u32", k_min3, 8},
+      {"v_and_or_b32", k_and_or, 8},   {"v_lshl_or_b32", k_lshl_or, 8}, {"v_alignbit_b32", k_alignbit, 8},
+      {"v_mul_lo_u32", k_mul_lo, 8},   {"v_cvt_f32_u32", k_cvt_f32, 4}, {"v_mul_f32", k_mul_f32, 4},
+      {"v_fma_f32", k_fma_f32, 8},     {"v_rcp_f32", k_rcp_f32, 4},
+      {"v_cndmask_b32", k_cndmask, 4}};
   hipDeviceProp_t prop;
   hipGetDeviceProperties(&prop, 0);
   const unsigned cus = prop.multiProcessorCount, threads = 256, iters = 2048;
@@ -48,7 +80,7 @@ int main() {
   hipEventCreate(&e1);
   printf("{\"cus\": %u, \"rates\": [", cus);
   bool first = true;
-  for (unsigned wps : {1u, 2u, 4u, 8u}) {  // waves per SIMD (4 waves per block, one block per SIMD-wave)
+  for (unsigned wps : {8u}) {  // waves per SIMD (4 waves per block, one block per SIMD-wave)
     for (unsigned i = 0; i < sizeof(ks) / sizeof(ks[0]); ++i) {
       const unsigned blocks = cus * wps;
       hipLaunchKernelGGL(ks[i].f, dim3(blocks), dim3(threads), 0, 0, out, 16u, 1u);

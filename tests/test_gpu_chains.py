@@ -1,0 +1,85 @@
+"""GPU parity of the ranking product, Search::sorted_evolving_configs
+(search.rs:97-178), whose superset / min_mean_decrease joins and final order
+run on the device (bote_evolving_chains), against the oracle's chains
+(tests/golden/chains.json, tests/golden/make_chain_golden.py)."""
+import json
+import os
+
+import pytest
+
+from fantoch_amd.bote import FTMetric, RankingParams, Search, SearchInput
+from fantoch_amd.planet import Planet
+
+pytestmark = pytest.mark.gpu
+CHAINS = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "chains.json")))
+_SEARCH = {}
+
+
+def _search(si):
+    if si not in _SEARCH:
+        _SEARCH[si] = Search(3, 13, si, planet=Planet.new())
+    return _SEARCH[si]
+
+
+def _names(chain):
+    return [[r.name for r in cs.config] for cs in chain]
+
+
+@pytest.mark.parametrize("case", ["R13C13_0", "R13C13_1", "R17C17_0", "R17C17_1", "R20C20_0", "R20C20_1"])
+def test_evolving_chains_vs_oracle(case):
+    g = CHAINS["cases"][case]
+    rp = RankingParams.new(*[int(x) for x in g["params"]], 3, 13, FTMetric.F1F2)
+    s = _search(SearchInput(g["input"]))
+    chains = s.sorted_evolving_configs(rp)
+    assert len(chains) == g["nchains"]
+    for (sc, chain, _), (gsc, gsets) in zip(chains, g["chains"]):
+        assert sc.value() == gsc
+        assert _names(chain) == gsets
+    arr = s.evolving_chain_arrays(rp)
+    assert sum(a["total"] for a in arr) == g["nchains"]
+    if arr:
+        assert s.chains_digest(arr[0]) == int(g["digest"])
+
+
+@pytest.mark.parametrize("case", ["R13C13_2", "R13C13_3", "R17C17_2", "R17C17_3"])
+def test_evolving_chains_lenient_digest(case):
+    """10^3..10^7 chains (lenient ranking params): every chain, in order, by
+    digest, plus the first K chains, against the oracle."""
+    g = CHAINS["cases"][case]
+    rp = RankingParams.new(*[int(x) for x in g["params"]], 3, 13, FTMetric.F1F2)
+    s = _search(SearchInput(g["input"]))
+    (arr,) = s.evolving_chain_arrays(rp)
+    assert arr["total"] == g["nchains"] and len(arr["score"]) == g["nchains"]
+    assert s.chains_digest(arr) == int(g["digest"])
+    head = s.sorted_evolving_configs(rp, limit=len(g["chains"]))
+    for (sc, chain, _), (gsc, gsets) in zip(head, g["chains"]):
+        assert sc.value() == gsc
+        assert _names(chain) == gsets
+
+
+@pytest.mark.parametrize("pi", [0, 1, 2])
+def test_evolving_chains_r17cmaxn(pi):
+    """Every one of R17CMaxN's 2,380 client sets searched on the device; the
+    oracle-sampled sets (every 20th) have the same chain count and first
+    chains, and the merged order is score-descending across sets."""
+    g = CHAINS["cases"][f"R17CMaxN_{pi}"]
+    rp = RankingParams.new(*[int(x) for x in g["params"]], 3, 13, FTMetric.F1F2)
+    s = _search(SearchInput.R17CMaxN)
+    assert len(s.all_configs) == g["sets"]
+    chains = s.sorted_evolving_configs(rp)
+    by_set = {}
+    for sc, chain, clients in chains:
+        by_set.setdefault(tuple(r.name for r in clients), []).append((sc, chain))
+    for e in g["per_set"]:
+        clients = tuple(r.name for r in s.all_configs[e["set"]][0])
+        got = by_set.get(clients, [])
+        assert len(got) == e["nchains"], e["set"]
+        for (sc, chain), (gsc, gsets) in zip(got, e["chains"]):
+            assert sc.value() == gsc
+            assert _names(chain) == gsets
+    for a in s.evolving_chain_arrays(rp):
+        e = next((x for x in g["per_set"] if x["set"] == a["ci"]), None)
+        if e is not None:
+            assert s.chains_digest(a) == int(e["digest"]), a["ci"]
+    vals = [sc for sc, _, _ in chains]
+    assert all(not (b > a) for a, b in zip(vals, vals[1:]))
