@@ -60,26 +60,24 @@ def test_evolving_chains_lenient_digest(case):
 @pytest.mark.parametrize("pi", [0, 1, 2])
 def test_evolving_chains_r17cmaxn(pi):
     """Every one of R17CMaxN's 2,380 client sets searched on the device; the
-    oracle-sampled sets (every 20th) have the same chain count and first
-    chains, and the merged order is score-descending across sets."""
+    oracle-sampled sets (every 20th) have the same chain count, first chains
+    and all-chain digest, and the merged order is score-descending across sets."""
     g = CHAINS["cases"][f"R17CMaxN_{pi}"]
     rp = RankingParams.new(*[int(x) for x in g["params"]], 3, 13, FTMetric.F1F2)
     s = _search(SearchInput.R17CMaxN)
     assert len(s.all_configs) == g["sets"]
-    chains = s.sorted_evolving_configs(rp)
-    by_set = {}
-    for sc, chain, clients in chains:
-        by_set.setdefault(tuple(r.name for r in clients), []).append((sc, chain))
+    arrs = {a["ci"]: a for a in s.evolving_chain_arrays(rp)}
     for e in g["per_set"]:
-        clients = tuple(r.name for r in s.all_configs[e["set"]][0])
-        got = by_set.get(clients, [])
-        assert len(got) == e["nchains"], e["set"]
-        for (sc, chain), (gsc, gsets) in zip(got, e["chains"]):
-            assert sc.value() == gsc
-            assert _names(chain) == gsets
-    for a in s.evolving_chain_arrays(rp):
-        e = next((x for x in g["per_set"] if x["set"] == a["ci"]), None)
-        if e is not None:
-            assert s.chains_digest(a) == int(e["digest"]), a["ci"]
-    vals = [sc for sc, _, _ in chains]
+        a = arrs.get(e["set"])
+        assert (a["total"] if a else 0) == e["nchains"], e["set"]
+        if not a:
+            continue
+        assert s.chains_digest(a) == int(e["digest"]), e["set"]
+        for k, (gsc, gsets) in enumerate(e["chains"]):
+            assert a["score"][k] == gsc
+            got = [[r.name for r in s._config_set(e["set"], 3 + 2 * lvl, int(a["idx"][k, lvl])).config]
+                   for lvl in range(6)]
+            assert got == gsets
+    head = s.sorted_evolving_configs(rp, limit=20)
+    vals = [sc for sc, _, _ in head]
     assert all(not (b > a) for a, b in zip(vals, vals[1:]))
