@@ -70,7 +70,8 @@ __host__ __device__ inline size_t group_layout(const FastArgs& a, int N, int NLW
   off[1] = o; o += (size_t)a.R * (a.cq_quads + 1) * 8;
   off[2] = o; o += a.rq_separate ? (size_t)a.R * (a.rq_quads + 1) * 8 : 0;
   off[3] = o; o += (size_t)a.ns * 4;  // srv
-  off[4] = o; o += (size_t)a.ns * 4;  // cs1
+  o = (o + 7) & ~(size_t)7;
+  off[4] = o; o += (size_t)a.ns * 8;  // lrec: (cs1, f32 vcol) per position
   o = (o + 15) & ~(size_t)15;
   off[5] = o; o += (size_t)a.ns * 8;                   // cs2
   off[6] = o; o += (size_t)a.ns * 8;                   // vcol (f64)
@@ -247,7 +248,7 @@ __global__ void __launch_bounds__(FAST_BD, BOTE_GROUP_WAVES) sweep_group_kernel(
   const uint32_t cqt = LB + (uint32_t)off[1];
   const uint32_t rqt = LB + (uint32_t)(a.rq_separate ? off[2] : off[1]);
   uint32_t* srv = (uint32_t*)(smem + off[3]);
-  uint32_t* cs1 = (uint32_t*)(smem + off[4]);
+  uint2* lrec = (uint2*)(smem + off[4]);  // per position: .x column sum S1, .y f32 bits of V
   uint64_t* cs2 = (uint64_t*)(smem + off[5]);
   double* vcol = (double*)(smem + off[6]);
   const uint64_t* binom = a.binom;
@@ -288,9 +289,10 @@ __global__ void __launch_bounds__(FAST_BD, BOTE_GROUP_WAVES) sweep_group_kernel(
       c1 += v;
       c2 += v * v;
     }
-    cs1[i] = (uint32_t)c1;
     cs2[i] = c2;
-    vcol[i] = (double)((uint64_t)a.nc * c2 - c1 * c1);  // exact: < 2^53
+    const double v = (double)((uint64_t)a.nc * c2 - c1 * c1);  // exact: < 2^53
+    vcol[i] = v;
+    lrec[i] = make_uint2((uint32_t)c1, __float_as_uint((float)v));
   }
   __syncthreads();
 
@@ -335,8 +337,9 @@ __global__ void __launch_bounds__(FAST_BD, BOTE_GROUP_WAVES) sweep_group_kernel(
         uint32_t pos = 0;
 #pragma unroll
         for (int k = 0; k < F; ++k) pos = lane == (uint32_t)k ? hq[k] : pos;
-        s32(fS1 + 4 * lane, cs1[pos]);
-        *(AS3 float*)(uintptr_t)(fVf + 4 * lane) = (float)vcol[pos];
+        const uint2 lr = lrec[pos];
+        s32(fS1 + 4 * lane, lr.x);
+        s32(fVf + 4 * lane, lr.y);
       }
       if (lane < (uint32_t)FP) {
         // rows 2*lane and 2*lane+1: sorted distances to the other fixed
@@ -468,54 +471,86 @@ __global__ void __launch_bounds__(FAST_BD, BOTE_GROUP_WAVES) sweep_group_kernel(
           //      group's packed sorted lists
 #pragma unroll
           for (int pp = 0; pp < FP; ++pp) {
-            uint32_t L[KQ];
+            us2 A[KQ];  // the group's sorted fixed-row lists (uniform)
 #pragma unroll
-            for (int i = 0; i < KQ; ++i) L[i] = l32(upk + (pp * KQ + i) * 4);
+            for (int i = 0; i < KQ; ++i) A[i] = as_us2(l32(upk + (pp * KQ + i) * 4));
             const bool has_hi = 2 * pp + 1 < F;
+            us2 y[3];  // the 3 lane distances, then sorted (3 compare-exchanges)
 #pragma unroll
             for (int m = 0; m < 3; ++m) {
-              if (ABLATE(a, 64)) break;
               const uint32_t lo = l16(cv[m] + 2 * freg[2 * pp]);
               const uint32_t hi = has_hi ? l16(cv[m] + 2 * freg[has_hi ? 2 * pp + 1 : 2 * pp]) : 0xFFF0u;
-              us2 x = as_us2((lo | (hi << 16)) >> LAT_SHIFT);
-              if (!has_hi) x = as_us2(as_u32(x) | 0xFFFF0000u);
+              y[m] = as_us2((lo | (hi << 16)) >> LAT_SHIFT);
+              if (!has_hi) y[m] = as_us2(as_u32(y[m]) | 0xFFFF0000u);
+            }
+            {
+              us2 t = pk_min(y[0], y[1]);
+              y[1] = pk_max(y[0], y[1]);
+              y[0] = t;
+              t = pk_min(y[1], y[2]);
+              y[2] = pk_max(y[1], y[2]);
+              y[1] = t;
+              t = pk_min(y[0], y[1]);
+              y[1] = pk_max(y[0], y[1]);
+              y[0] = t;
+            }
+            // merge: the k-th smallest of A u y is the min over the splits
+            // (k+1-j from A, j from y) of max(A[k-j], y[j-1])
+            uint32_t L[KQ];
 #pragma unroll
-              for (int i = 0; i < KQ; ++i) {
-                const us2 li = as_us2(L[i]);
-                L[i] = as_u32(pk_min(li, x));
-                if (i + 1 < KQ) x = pk_max(li, x);
+            for (int k = 0; k < KQ; ++k) {
+              us2 z = A[k];
+#pragma unroll
+              for (int j = 1; j <= 3 && j <= k + 1; ++j) {
+                const int i = k + 1 - j;  // elements taken from A
+                z = pk_min(z, i == 0 ? y[j - 1] : pk_max(A[i > 0 ? i - 1 : 0], y[j - 1]));
               }
+              L[k] = as_u32(z);
             }
             emit_pk(3 + 2 * pp, has_hi, L);
           }
           // ---- FPaxos leader (f = 1, q = 2, min COV, first in config order)
           auto pos_of = [&](int l) { return l < 3 ? pv[l] : hq[l - 3]; };
           auto reg_of = [&](int l) { return l < 3 ? rv[l] : freg[l - 3]; };
-          auto s1_of = [&](int l) { return l < 3 ? cs1[pv[l]] : l32(fS1 + 4 * (l - 3)); };
-          auto vf_of = [&](int l) { return l < 3 ? (float)vcol[pv[l]] : lf32(fVf + 4 * (l - 3)); };
+          uint2 vrec[3];  // the variable members' (S1, f32 V): one 8-byte LDS read each
+#pragma unroll
+          for (int i = 0; i < 3; ++i) vrec[i] = lrec[pv[i]];
+          auto s1_of = [&](int l) { return l < 3 ? vrec[l].x : l32(fS1 + 4 * (l - 3)); };
+          auto vf_of = [&](int l) { return l < 3 ? __uint_as_float(vrec[l].y) : lf32(fVf + 4 * (l - 3)); };
           // COV^2 proxy r = V / S^2 per member in f32 (V one rounding, S
           // exact below 2^24, S^2 and the reciprocal one each): within 2^-22
           // of exact, so comparisons outside a 2^-18 band are decided; any
           // closer call re-runs the scan exactly (cov2_sign) or defers.
+          // Decided without a sequential scan: m = min r (a tree), the
+          // leader is the first member at m, and the decision is ambiguous
+          // when m > 0 and another member lies within the 2^-18 band above m
+          // (exact zeros, V = 0, tie exactly and keep the first, as the
+          // reference's first-minimum does).
           uint32_t bi = 0;
           bool amb = false;
           if (!ABLATE(a, 128)) {
             float rl[N];
 #pragma unroll
             for (int l = 0; l < N; ++l) {
-              const float fs = (float)(s1_of(l) + nc * Q2[l]);
+              const float fs = (float)(s1_of(l) + __umul24(nc, Q2[l]));
               rl[l] = vf_of(l) * __builtin_amdgcn_rcpf(fs * fs);
             }
-            float rb = rl[0];
+            float mn[N];
 #pragma unroll
-            for (int l = 1; l < N; ++l) {
-              const float r = rl[l];
-              const bool lt = r < rb * (1.0f - 0x1p-18f);
-              const bool near = !lt && r <= rb * (1.0f + 0x1p-18f) && (r > 0.0f || rb > 0.0f);
-              amb = amb || near;
-              bi = lt ? (uint32_t)l : bi;
-              rb = lt ? r : rb;
+            for (int l = 0; l < N; ++l) mn[l] = rl[l];
+#pragma unroll
+            for (int w = 1; w < N; w <<= 1)
+#pragma unroll
+              for (int l = 0; l + w < N; l += 2 * w) mn[l] = fminf(mn[l], mn[l + w]);
+            const float m = mn[0], lim = m * (1.0f + 0x1p-18f);
+            uint32_t eq = 0, nearm = 0;
+#pragma unroll
+            for (int l = 0; l < N; ++l) {
+              eq |= (rl[l] == m ? 1u : 0u) << l;
+              nearm |= (rl[l] <= lim ? 1u : 0u) << l;
             }
+            bi = (uint32_t)__builtin_ctz(eq);
+            amb = m > 0.0f && __builtin_popcount(nearm) > 1;
           }
           if (amb) {  // exact re-scan in the generic path's arithmetic
             amb = false;
@@ -656,7 +691,7 @@ __global__ void __launch_bounds__(FAST_BD, BOTE_GROUP_WAVES) sweep_group_kernel(
               mom[SLOT_E] = Mom{S1[QC::idx_e], S2[QC::idx_e], nc};
             }
             // ---- Input FPaxos from the leader column's sums
-            const uint32_t lc1 = cs1[lpos];
+            const uint32_t lc1 = lrec[lpos].x;
             const uint64_t lc2 = cs2[lpos];
             mom[SLOT_FF1] = leader_mom(lc1, lc2, nc, lq2);
             mom[SLOT_FF2] = leader_mom(lc1, lc2, nc, lq3);
