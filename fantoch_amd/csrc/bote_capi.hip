@@ -751,6 +751,9 @@ int bote_sweep_create_ex(const bote_planet* p, const uint32_t* servers, uint32_t
     for (auto v : p->lat) maxlat = std::max<uint32_t>(maxlat, v);
     const uint64_t amax = 2ull * maxlat, per_quad = 4 * amax * amax;
     f.s2_flush = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(1u << 20, per_quad ? 0xFFFFFFFFull / per_quad : 1u << 20));
+    // packed-u16 sums (group kernel): each half gains <= 2 * amax per quad
+    const uint64_t s1_flush = amax ? 0xFFFFull / (2 * amax) : 1u << 20;
+    f.g_flush = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(f.s2_flush, s1_flush));
     f.want_score = a.want_score;
     f.p_fmean = a.p_fmean;
     f.p_emean = a.p_emean;

@@ -591,15 +591,18 @@ __global__ void __launch_bounds__(FAST_BD, BOTE_GROUP_WAVES) sweep_group_kernel(
             Mom mom[NSLOT];
             // ---- Input leaderless: 3 lane columns + the wave's nearest-fixed line
             {
-              const us2 ones = {1, 1};
               const us2 J1 = {1, 1}, J2 = {2, 2};
-              uint32_t S1[NL], s2[NL];
+              // Sums use full-rate 32-bit adds on packed u16 pairs (no half
+              // overflows: lat + q < 2^15, and p1 is flushed every g_flush
+              // quads), squares the 2-wide dot product (s2, flushed to 64 bits)
+              uint32_t S1[NL], s2[NL], p1[NL];
               uint64_t S2[NL];
 #pragma unroll
               for (int t = 0; t < NL; ++t) {
                 S1[t] = 0;
                 S2[t] = 0;
                 s2[t] = 0;
+                p1[t] = 0;
               }
               const uint32_t c0 = cqt + rv[0] * cstride, c1 = cqt + rv[1] * cstride, c2 = cqt + rv[2] * cstride;
               // (m << GQSH) + qlane in one instruction (the compiler would
@@ -621,13 +624,12 @@ __global__ void __launch_bounds__(FAST_BD, BOTE_GROUP_WAVES) sweep_group_kernel(
                 const uint32_t a2 = qaddr(H & 15u), a3 = qaddr(__builtin_amdgcn_ubfe(H, 16, 4));
                 const us2 dlo = lo >> (us2)4, dhi = hi >> (us2)4;
                 auto acc1 = [&](int t, us2 q01, us2 q23) {
-                  us2 a01 = dlo + q01, a23 = dhi + q23;
-                  a01 = as_us2(as_u32(a01) & mlo);
-                  a23 = as_us2(as_u32(a23) & mhi);
-                  S1[t] = __builtin_amdgcn_udot2(a01, ones, S1[t], false);
-                  S1[t] = __builtin_amdgcn_udot2(a23, ones, S1[t], false);
-                  s2[t] = __builtin_amdgcn_udot2(a01, a01, s2[t], false);
-                  s2[t] = __builtin_amdgcn_udot2(a23, a23, s2[t], false);
+                  // packed adds as one 32-bit add: no carry crosses the halves
+                  const uint32_t a01 = (as_u32(dlo) + as_u32(q01)) & mlo;
+                  const uint32_t a23 = (as_u32(dhi) + as_u32(q23)) & mhi;
+                  p1[t] += a01 + a23;
+                  s2[t] = __builtin_amdgcn_udot2(as_us2(a01), as_us2(a01), s2[t], false);
+                  s2[t] = __builtin_amdgcn_udot2(as_us2(a23), as_us2(a23), s2[t], false);
                 };
                 // (16-bit loads into packed halves would need d16 loads, which
                 //  gfx950 with sramecc does not preserve; read words and perm)
@@ -648,15 +650,17 @@ __global__ void __launch_bounds__(FAST_BD, BOTE_GROUP_WAVES) sweep_group_kernel(
                 for (int t = 0; t < NL; ++t) {
                   S2[t] += s2[t];
                   s2[t] = 0;
+                  S1[t] += (p1[t] & 0xFFFFu) + (p1[t] >> 16);
+                  p1[t] = 0;
                 }
               };
               const uint32_t nql = ABLATE(a, 1) ? 0u : nq;
               // 4 quads per iteration (constant offsets fold into the ds_read
               // offset fields); s2 is flushed to 64 bits every s2_flush quads
               {
-                const uint32_t f4 = a.s2_flush >> 2 ? a.s2_flush >> 2 : 1u;
+                const uint32_t f4 = a.g_flush >> 2 ? a.g_flush >> 2 : 1u;
                 uint32_t g = 0, k = 0;
-                if (a.s2_flush >= 4) {
+                if (a.g_flush >= 4) {
                   for (; g + 4 <= nql; g += 4) {
                     quad(g * 8, ~0u, ~0u);
                     quad(g * 8 + 8, ~0u, ~0u);
@@ -669,8 +673,8 @@ __global__ void __launch_bounds__(FAST_BD, BOTE_GROUP_WAVES) sweep_group_kernel(
                   }
                   flush();
                 }
-                for (uint32_t g0 = g; g0 < nql; g0 += a.s2_flush) {
-                  const uint32_t ge = min(nql, g0 + a.s2_flush);
+                for (uint32_t g0 = g; g0 < nql; g0 += a.g_flush) {
+                  const uint32_t ge = min(nql, g0 + a.g_flush);
                   for (g = g0; g < ge; ++g) quad(g * 8, ~0u, ~0u);
                   flush();
                 }

@@ -89,6 +89,7 @@ struct FastArgs {
   uint64_t rb, re;
   uint32_t runlen;
   uint32_t s2_flush;  // quads per 32-bit sum-of-squares chunk
+  uint32_t g_flush;   // group kernel: quads per flush of its 32-bit square sums and packed-u16 sums
   int want_score, p_int;
   int64_t p1i, p2i;  // p_int: min_mean_{fpaxos,epaxos}_improv * nc as integers
   double p_fmean, p_emean;
