@@ -211,3 +211,32 @@ def test_tempo_quorum_sizes_known_answers():
             assert Protocol.Tempo.quorum_size(n, f) == tempo_quorum_sizes(n, f, False)[0]
             assert Protocol.TempoTiny.quorum_size(n, f) == tempo_quorum_sizes(n, f, True)[0]
             assert Protocol.TempoWrite.quorum_size(n, f) == tempo_quorum_sizes(n, f, True)[1]
+
+
+def test_write_dat_round_trip(tmp_path):
+    """write_dat is the inverse of Dat::latencies (planet/dat.rs:33-75) on
+    integral planets: every region's file re-read by Planet.from_dir gives the
+    same matrix and name order (GCP, AWS 2021 and a synthetic planet with
+    asymmetric pairs); each line is ping's `min/avg/max/mdev:zone` and the
+    lines are in the order `sort -n` gives them (ping_exp_gcp/region_ping_loop.sh,
+    run by fantoch_exp/src/bin/ping.rs:178-214)."""
+    import subprocess
+
+    from fantoch_amd.planet import AWS_2021_DIR, Planet, write_dat
+
+    for name, p in (("gcp", Planet.new()), ("aws", Planet.from_dir(AWS_2021_DIR)),
+                    ("syn", Planet.synthetic(24))):
+        d = tmp_path / name
+        for r in p.names:
+            path = write_dat(p, r, str(d))
+            lines = open(path).read().splitlines()
+            assert len(lines) == p.R
+            for ln in lines:
+                stats, zone = ln.rsplit(":", 1)
+                assert len(stats.split("/")) == 4 and zone in p.names
+            srt = subprocess.run(["sort", "-n", path], capture_output=True, text=True, check=True,
+                                 env={"LC_ALL": "C"}).stdout.splitlines()
+            assert srt == lines
+        q = Planet.from_dir(str(d))
+        assert q.names == p.names
+        assert np.array_equal(q.lat, p.lat)
