@@ -794,6 +794,12 @@ int bote_sweep_create_ex(const bote_planet* p, const uint32_t* servers, uint32_t
       if (!lt.empty() && hipMemcpy(s->lowtab.p, lt.data(), lt.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
         return cleanup(fail(BOTE_E_DEVICE, "upload group low table"));
       f.lowtab = s->lowtab.as<uint32_t>();
+      // workgroup size: 256 threads (4 waves).  Larger workgroups (which
+      // share the client-quad matrix, so R = 128 fits more waves per CU) were
+      // measured slower: R=128 n=6 at 640 threads, 5 waves/SIMD, 369 ms vs
+      // 348 ms at 256 threads, 2 waves/SIMD.
+      f.gbd = bote::FAST_BD;
+      f.gqsh = 10;
       const size_t gshm = bote::group_smem_bytes(f, n);
       // bote.py DEFAULT_OBJECTIVES: SCORE, MEAN af1, MEAN ff1, COV af1, MEAN e
       static const uint32_t dk[5] = {BOTE_OBJ_SCORE, BOTE_OBJ_MEAN, BOTE_OBJ_MEAN, BOTE_OBJ_COV, BOTE_OBJ_MEAN};
@@ -804,7 +810,7 @@ int bote_sweep_create_ex(const bote_planet* p, const uint32_t* servers, uint32_t
       if (gshm <= device_max_lds(p->device)) {
         s->group = true;
         s->fshm = gshm;
-        s->fgrid = (uint32_t)(device_cus(p->device) * bote::group_occupancy(n, gshm, s->def_obj));
+        s->fgrid = (uint32_t)(device_cus(p->device) * std::max(1, bote::group_occupancy(n, gshm, s->def_obj, f.gbd)));
       }
     }
   }
@@ -1062,7 +1068,7 @@ int bote_sweep_deferred(bote_sweep* s, void* hip_stream, uint64_t* out) {
 int bote_sweep_grid(const bote_sweep* s, uint32_t* out_grid, uint32_t* out_block, uint32_t* out_lds_bytes) {
   if (!s) return fail(BOTE_E_ARG, "sweep is null");
   if (out_grid) *out_grid = s->fast ? s->fgrid : s->grid;
-  if (out_block) *out_block = s->fast ? bote::FAST_BD : s->bd;
+  if (out_block) *out_block = s->fast ? (s->group ? s->fargs.gbd : bote::FAST_BD) : s->bd;
   if (out_lds_bytes) *out_lds_bytes = (uint32_t)(s->fast ? s->fshm : s->shm);
   return BOTE_OK;
 }

@@ -37,14 +37,16 @@
 
 namespace bote {
 
-constexpr int WPB = FAST_BD / 64;  // wavefronts per workgroup
+// Workgroup size: a.gbd threads (a multiple of 64, <= GROUP_MAX_BD), chosen on
+// the host so that LDS does not cap the waves per SIMD (R = 128 needs larger
+// workgroups than R = 64: the client-quad matrix is shared per workgroup).
+constexpr int GROUP_MAX_BD = 1024;
 // waves per SIMD the register allocation targets (5: <= 96 VGPRs; LDS per
 // workgroup stays under 32 KB at R = 64, so 5 workgroups fit a CU)
 #ifndef BOTE_GROUP_WAVES
 #define BOTE_GROUP_WAVES 5
 #endif
-constexpr uint32_t GQSH = 10;      // log2(FAST_BD * 4): byte stride between qtab member planes
-static_assert((1u << GQSH) == FAST_BD * 4, "qtab plane stride");
+// qtab member planes are 1 << a.gqsh bytes apart (>= gbd * 4, a power of two)
 
 __host__ __device__ constexpr int cmax(int a, int b) { return a > b ? a : b; }
 
@@ -66,7 +68,7 @@ __host__ __device__ inline uint32_t gline_bytes(const FastArgs& a, int N, int KQ
 
 __host__ __device__ inline size_t group_layout(const FastArgs& a, int N, int NLW, int KQ, size_t* off) {
   size_t o = 0;
-  off[0] = o; o += (size_t)N * FAST_BD * NLW * 4;  // qtab first: offsets stay small
+  off[0] = o; o += ((size_t)N * NLW) << a.gqsh;  // qtab first: offsets stay small
   off[1] = o; o += (size_t)a.R * (a.cq_quads + 1) * 8;
   off[2] = o; o += a.rq_separate ? (size_t)a.R * (a.rq_quads + 1) * 8 : 0;
   off[3] = o; o += (size_t)a.ns * 4;  // srv
@@ -76,7 +78,7 @@ __host__ __device__ inline size_t group_layout(const FastArgs& a, int N, int NLW
   off[5] = o; o += (size_t)a.ns * 8;                   // cs2
   off[6] = o; o += (size_t)a.ns * 8;                   // vcol (f64)
   off[7] = o;  // (binomials stay in global memory: uniform scalar loads, once per group)
-  off[8] = o; o += (size_t)WPB * gline_bytes(a, N, KQ);  // per-wave group lines
+  off[8] = o; o += (size_t)(a.gbd / 64) * gline_bytes(a, N, KQ);  // per-wave group lines
   o = (o + 15) & ~(size_t)15;
   off[9] = o; o += (size_t)a.n_obj * KP * 16;  // top
   off[10] = o; o += (size_t)64 * 16;          // cand (one wave's candidates)
@@ -230,7 +232,7 @@ __device__ __forceinline__ int cov2_sign(float Vx, uint32_t Sx, float Vy, uint32
 // MEAN ff1, COV af1, MEAN e), compiled in; otherwise the objectives come from
 // the arguments (finish_config, bote_fast.hpp).
 template <int N, bool DEF>
-__global__ void __launch_bounds__(FAST_BD, BOTE_GROUP_WAVES) sweep_group_kernel(FastArgs a) {
+__global__ void __launch_bounds__(GROUP_MAX_BD, BOTE_GROUP_WAVES) sweep_group_kernel(FastArgs a) {
   using QC = QCfg<N>;
   using GC = GCfg<N>;
   constexpr int NL = QC::NL;
@@ -259,29 +261,30 @@ __global__ void __launch_bounds__(FAST_BD, BOTE_GROUP_WAVES) sweep_group_kernel(
   tk.thr = (Rec*)(smem + off[12]);
   tk.cnt = nullptr;
   int* lock = (int*)(smem + off[13]);
-  const uint32_t tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, BD = blockDim.x, WPB = BD >> 6;
+  const uint32_t qsh = a.gqsh;  // log2 of the qtab plane stride (bytes)
 
   // ---- stage: quad matrices, server list, binomials; then per-position sums
   {
     const uint32_t cw = a.R * (a.cq_quads + 1) * 2;
     const uint32_t* src = (const uint32_t*)a.cqt;
     uint32_t* dst = (uint32_t*)(smem + off[1]);
-    for (uint32_t i = tid; i < cw; i += FAST_BD) dst[i] = src[i];
+    for (uint32_t i = tid; i < cw; i += BD) dst[i] = src[i];
     if (a.rq_separate) {
       const uint32_t rw = a.R * (a.rq_quads + 1) * 2;
       const uint32_t* rs = (const uint32_t*)a.rqt;
       uint32_t* rd = (uint32_t*)(smem + off[2]);
-      for (uint32_t i = tid; i < rw; i += FAST_BD) rd[i] = rs[i];
+      for (uint32_t i = tid; i < rw; i += BD) rd[i] = rs[i];
     }
   }
-  for (uint32_t i = tid; i < a.ns; i += FAST_BD) srv[i] = a.srv[i];
-  for (uint32_t i = tid; i < (uint32_t)a.n_obj * KP; i += FAST_BD) tk.top[i] = rec_max();
+  for (uint32_t i = tid; i < a.ns; i += BD) srv[i] = a.srv[i];
+  for (uint32_t i = tid; i < (uint32_t)a.n_obj * KP; i += BD) tk.top[i] = rec_max();
   if (tid < MAXOBJ) tk.thr[tid] = rec_max();
   if (tid == 0) *lock = 0;
   __syncthreads();
   const uint32_t cstride = (a.cq_quads + 1) * 8;  // bytes per CQT column
   const uint32_t rstride = (a.rq_quads + 1) * 8;
-  for (uint32_t i = tid; i < a.ns; i += FAST_BD) {
+  for (uint32_t i = tid; i < a.ns; i += BD) {
     const uint32_t col = cqt + srv[i] * cstride;
     uint64_t c1 = 0, c2 = 0;
     for (uint32_t c = 0; c < a.nc; ++c) {
@@ -424,7 +427,7 @@ __global__ void __launch_bounds__(FAST_BD, BOTE_GROUP_WAVES) sweep_group_kernel(
               Q2[j + h] = (L[0] >> sh) & 0xFFFFu;
               Q3[j + h] = (L[1] >> sh) & 0xFFFFu;
               const uint32_t word = NL >= 2 ? __builtin_amdgcn_perm(w1, w0, sel) : ((w0 >> sh) & 0xFFFFu);
-              s32(qlane + ((uint32_t)(j + h) << GQSH), word);
+              s32(qlane + ((uint32_t)(j + h) << qsh), word);
               cS1p += word;
               const uint32_t q0 = word & 0xFFFFu;
               cS2[0] += q0 * q0;
@@ -434,7 +437,7 @@ __global__ void __launch_bounds__(FAST_BD, BOTE_GROUP_WAVES) sweep_group_kernel(
               }
               if (NL == 3) {
                 const uint32_t q2 = (L[QC::lq(NL - 1) - 2] >> sh) & 0xFFFFu;
-                s32(qlane + ((uint32_t)(N + j + h) << GQSH), q2);
+                s32(qlane + ((uint32_t)(N + j + h) << qsh), q2);
                 cS1e += q2;
                 cS2[NL - 1] += q2 * q2;
               }
@@ -605,11 +608,11 @@ __global__ void __launch_bounds__(FAST_BD, BOTE_GROUP_WAVES) sweep_group_kernel(
                 p1[t] = 0;
               }
               const uint32_t c0 = cqt + rv[0] * cstride, c1 = cqt + rv[1] * cstride, c2 = cqt + rv[2] * cstride;
-              // (m << GQSH) + qlane in one instruction (the compiler would
+              // (m << qsh) + qlane in one instruction (the compiler would
               // otherwise re-associate it into shift, and, add)
               auto qaddr = [&](uint32_t m) {
                 uint32_t r;
-                asm("v_lshl_add_u32 %0, %1, 10, %2" : "=v"(r) : "v"(m), "v"(qlane));
+                asm("v_lshl_add_u32 %0, %1, %2, %3" : "=v"(r) : "v"(m), "s"(qsh), "v"(qlane));
                 return r;
               };
               auto quad = [&](uint32_t g8, uint32_t mlo, uint32_t mhi) {
@@ -639,7 +642,7 @@ __global__ void __launch_bounds__(FAST_BD, BOTE_GROUP_WAVES) sweep_group_kernel(
                   acc1(NL >= 2 ? 1 : 0, as_us2(__builtin_amdgcn_perm(w1, w0, 0x07060302u)),
                        as_us2(__builtin_amdgcn_perm(w3, w2, 0x07060302u)));
                 if (NL == 3) {
-                  constexpr uint32_t P2 = (uint32_t)N << GQSH;
+                  const uint32_t P2 = (uint32_t)N << qsh;
                   const uint32_t x0 = l32(a0 + P2), x1 = l32(a1 + P2), x2 = l32(a2 + P2), x3 = l32(a3 + P2);
                   acc1(NL - 1, as_us2(__builtin_amdgcn_perm(x1, x0, 0x05040100u)),
                        as_us2(__builtin_amdgcn_perm(x3, x2, 0x05040100u)));
@@ -878,7 +881,7 @@ __global__ void __launch_bounds__(FAST_BD, BOTE_GROUP_WAVES) sweep_group_kernel(
   if (digest) atomicAdd(&a.out_counters[1], (unsigned long long)digest);
   __syncthreads();
   Rec* dst = a.out_top + (size_t)blockIdx.x * a.n_obj * KP;
-  for (uint32_t i = tid; i < (uint32_t)a.n_obj * KP; i += FAST_BD) dst[i] = tk.top[i];
+  for (uint32_t i = tid; i < (uint32_t)a.n_obj * KP; i += BD) dst[i] = tk.top[i];
 }
 
 // ------------------------------------------------------------- launcher ---
@@ -887,7 +890,7 @@ static hipError_t launch_group_n(const FastArgs& a, uint32_t grid, size_t shm, h
   auto k = sweep_group_kernel<N, DEF>;
   hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k, dim3(grid), dim3(FAST_BD), shm, st, a);
+  hipLaunchKernelGGL(k, dim3(grid), dim3(a.gbd), shm, st, a);
   return hipGetLastError();
 }
 
@@ -902,13 +905,13 @@ static const void* group_fn(uint32_t n, bool def) {
   }
 }
 
-int group_occupancy(uint32_t n, size_t shm, bool def) {
+int group_occupancy(uint32_t n, size_t shm, bool def, uint32_t bd) {
   int nb = 0;
   const void* k = group_fn(n, def);
   if (!k) return 0;
-  if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm) != hipSuccess) return 1;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, (int)FAST_BD, shm) != hipSuccess) return 1;
-  return nb > 0 ? nb : 1;
+  if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm) != hipSuccess) return 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, (int)bd, shm) != hipSuccess) return 0;
+  return nb > 0 ? nb : 0;
 }
 
 hipError_t launch_group(const FastArgs& a, uint32_t n, bool def, uint32_t grid, size_t shm, hipStream_t st) {

@@ -90,6 +90,8 @@ struct FastArgs {
   uint32_t runlen;
   uint32_t s2_flush;  // quads per 32-bit sum-of-squares chunk
   uint32_t g_flush;   // group kernel: quads per flush of its 32-bit square sums and packed-u16 sums
+  uint32_t gbd;       // group kernel: workgroup size (multiple of 64, <= 1024)
+  uint32_t gqsh;      // group kernel: log2 of the qtab plane stride in bytes (1 << gqsh >= gbd * 4)
   int want_score, p_int;
   int64_t p1i, p2i;  // p_int: min_mean_{fpaxos,epaxos}_improv * nc as integers
   double p_fmean, p_emean;
@@ -126,7 +128,7 @@ size_t fast_smem_bytes(const FastArgs& a, uint32_t n);
 int fast_occupancy(uint32_t n, size_t shm);
 hipError_t launch_fast(const FastArgs& a, uint32_t n, uint32_t grid, size_t shm, hipStream_t st);
 size_t group_smem_bytes(const FastArgs& a, uint32_t n);
-int group_occupancy(uint32_t n, size_t shm, bool def_objectives);
+int group_occupancy(uint32_t n, size_t shm, bool def_objectives, uint32_t bd);
 hipError_t launch_group(const FastArgs& a, uint32_t n, bool def_objectives, uint32_t grid, size_t shm, hipStream_t st);
 
 size_t eval_smem_bytes(const EvalArgs& a, uint32_t n, uint32_t bd, bool topk);
