@@ -679,26 +679,47 @@ uint32_t oracle_quorum_size(int proto, uint32_t n, uint32_t f) {
 //               values, then Colocated slots 5..9 each n values); missing
 //               slots (n < 4: af2/ff2) are filled with ~0.
 //   out_leader: ncfg leader positions inside the config
-int oracle_compute_stats(void* h, const uint32_t* configs, uint32_t ncfg, uint32_t n,
-                         const uint32_t* clients, uint32_t nc, uint64_t* out_vals,
-                         uint32_t* out_leader) {
+//   threads:    std::thread workers over contiguous config chunks
+int oracle_compute_stats_mt(void* h, const uint32_t* configs, uint32_t ncfg, uint32_t n,
+                            const uint32_t* clients, uint32_t nc, uint64_t* out_vals,
+                            uint32_t* out_leader, uint32_t threads) {
   ORACLE_TRY
   Bote b{(Planet*)h};
   std::vector<uint32_t> cl(clients, clients + nc);
   size_t stride = 5 * (size_t)nc + 5 * (size_t)n;
-  for (uint32_t i = 0; i < ncfg; ++i) {
-    std::vector<uint32_t> cfg(configs + (size_t)i * n, configs + (size_t)(i + 1) * n);
-    ProtocolStats st;
-    compute_stats(b, cfg, cl, st);
-    uint64_t* o = out_vals + stride * i;
-    for (int s = 0; s < NKEYS; ++s) {
-      size_t len = s < 5 ? nc : n;
-      size_t off = s < 5 ? (size_t)s * nc : 5 * (size_t)nc + (size_t)(s - 5) * n;
-      for (size_t k = 0; k < len; ++k) o[off + k] = st.has[s] ? st.raw[s][k] : ~0ull;
+  if (threads == 0) threads = 1;
+  std::vector<std::string> errs(threads);
+  auto work = [&](uint32_t t) {
+    try {
+      for (uint64_t i = (uint64_t)ncfg * t / threads; i < (uint64_t)ncfg * (t + 1) / threads; ++i) {
+        std::vector<uint32_t> cfg(configs + i * n, configs + (i + 1) * n);
+        ProtocolStats st;
+        compute_stats(b, cfg, cl, st);
+        uint64_t* o = out_vals + stride * i;
+        for (int s = 0; s < NKEYS; ++s) {
+          size_t len = s < 5 ? nc : n;
+          size_t off = s < 5 ? (size_t)s * nc : 5 * (size_t)nc + (size_t)(s - 5) * n;
+          for (size_t k = 0; k < len; ++k) o[off + k] = st.has[s] ? st.raw[s][k] : ~0ull;
+        }
+        out_leader[i] = (uint32_t)st.leader_pos;
+      }
+    } catch (const std::exception& ex) {
+      errs[t] = ex.what();
     }
-    out_leader[i] = (uint32_t)st.leader_pos;
-  }
+  };
+  std::vector<std::thread> pool;
+  for (uint32_t t = 1; t < threads; ++t) pool.emplace_back(work, t);
+  work(0);
+  for (auto& th : pool) th.join();
+  for (auto& e : errs)
+    if (!e.empty()) throw Panic(e);
   ORACLE_CATCH
+}
+
+int oracle_compute_stats(void* h, const uint32_t* configs, uint32_t ncfg, uint32_t n,
+                         const uint32_t* clients, uint32_t nc, uint64_t* out_vals,
+                         uint32_t* out_leader) {
+  return oracle_compute_stats_mt(h, configs, ncfg, n, clients, nc, out_vals, out_leader, 1);
 }
 
 // compute_score (search.rs:421-472) for a batch of explicit configs.

@@ -65,6 +65,8 @@ def lib():
         L.oracle_quorum_size.argtypes = [C.c_int, C.c_uint32, C.c_uint32]
         L.oracle_compute_stats.argtypes = [C.c_void_p, u32p, C.c_uint32, C.c_uint32, u32p, C.c_uint32,
                                            u64p, u32p]
+        L.oracle_compute_stats_mt.argtypes = [C.c_void_p, u32p, C.c_uint32, C.c_uint32, u32p, C.c_uint32,
+                                              u64p, u32p, C.c_uint32]
         L.oracle_scores.argtypes = [C.c_void_p, u32p, C.c_uint32, C.c_uint32, u32p, C.c_uint32, f64p, C.c_int,
                                     f64p, np.ctypeslib.ndpointer(np.uint8, flags="C_CONTIGUOUS")]
         L.oracle_colex_unrank.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32, u32p]
@@ -151,15 +153,15 @@ class OraclePlanet:
         _check(lib().oracle_best_leader(self.h, s, len(s), c, len(c), q, stat, C.byref(out)))
         return out.value
 
-    def compute_stats(self, configs: np.ndarray, clients) -> Tuple[np.ndarray, np.ndarray]:
+    def compute_stats(self, configs: np.ndarray, clients, threads: int = 1) -> Tuple[np.ndarray, np.ndarray]:
         """configs: (ncfg, n) region ids. Returns (vals (ncfg, 5*nc+5*n) u64, leader_pos)."""
         cfg = _u32(configs)
         ncfg, n = cfg.shape
         c = _u32(clients)
         vals = np.zeros((ncfg, 5 * len(c) + 5 * n), np.uint64)
         lead = np.zeros(ncfg, np.uint32)
-        _check(lib().oracle_compute_stats(self.h, cfg.reshape(-1), ncfg, n, c, len(c),
-                                          vals.reshape(-1), lead))
+        _check(lib().oracle_compute_stats_mt(self.h, cfg.reshape(-1), ncfg, n, c, len(c),
+                                             vals.reshape(-1), lead, threads))
         return vals, lead
 
     def scores(self, configs: np.ndarray, clients, rparams, ft_metric: int = 2):
