@@ -2,9 +2,11 @@
 gloo on CPU: world sizes 2, 3 and 9 (9 exercises the merge tree), each rank a
 separate process sweeping its contiguous rank shard through the oracle-backed
 stand-in (tests/oracle_sweep.py).  The merged top-K, valid count and digest
-must equal one unsharded sweep.  The GPU path (device blocks, RCCL) runs the
+must equal one unsharded sweep and the committed oracle fixture
+(tests/golden/topk.json, gcp_n5: the full C(20, 5) rank space).  The GPU path (device blocks, RCCL) runs the
 same code with backend "nccl" in bench.py; tests/test_gpu_parity.py checks
 its device merge against shard-count independence."""
+import json
 import os
 import socket
 import sys
@@ -69,9 +71,15 @@ def test_sharded_sweep_gloo_equals_unsharded(world):
     for p in procs:
         p.join(60)
         assert p.exitcode == 0
+    fx = json.load(open(os.path.join(ROOT, "tests", "golden", "topk.json")))["cases"]["gcp_n5"]
+    assert (int(fx["rank_begin"]), int(fx["rank_end"])) == (0, sw.total)
     for rank, tops, valid, digest in got:
         assert tops == want.tops, f"rank {rank}: merged top-K differs from the unsharded sweep"
         assert (valid, digest) == (want.valid, want.digest)
+        assert (valid, digest) == (int(fx["valid"]), int(fx["digest"])), f"rank {rank}: differs from the fixture"
+        for o, lst in enumerate(tops):
+            assert len(lst) == K
+            assert [(k, r) for k, r in lst] == [(int(k), r) for k, r in fx["tops"][o][:len(lst)]]
 
 
 def test_shard_range_partition():
