@@ -800,13 +800,26 @@ int bote_sweep_create_ex(const bote_planet* p, const uint32_t* servers, uint32_t
       // 348 ms at 256 threads, 2 waves/SIMD.
       f.gbd = bote::FAST_BD;
       f.gqsh = 10;
-      const size_t gshm = bote::group_smem_bytes(f, n);
+      f.gslots = 0;
       // bote.py DEFAULT_OBJECTIVES: SCORE, MEAN af1, MEAN ff1, COV af1, MEAN e
       static const uint32_t dk[5] = {BOTE_OBJ_SCORE, BOTE_OBJ_MEAN, BOTE_OBJ_MEAN, BOTE_OBJ_COV, BOTE_OBJ_MEAN};
       static const uint32_t ds[5] = {0, BOTE_SLOT_AF1, BOTE_SLOT_FF1, BOTE_SLOT_AF1, BOTE_SLOT_E};
       s->def_obj = n_obj == 5 && f.want_score;
       for (uint32_t o = 0; s->def_obj && o < 5; ++o)
         s->def_obj = objs[o].kind == dk[o] && (dk[o] == BOTE_OBJ_SCORE || objs[o].slot == ds[o]);
+      if (bote::group_uses_lines(n)) {
+        // client lines per wave: as many (<= 16) as keep the workgroups per
+        // CU of the kernel without lines (a step has 7.7 distinct (p1, p2)
+        // on average at R=64 n=7, 4.0 at R=128 n=6)
+        const int occ0 = bote::group_occupancy(n, bote::group_smem_bytes(f, n), s->def_obj, f.gbd);
+        for (uint32_t sl = 16; sl >= 1; --sl) {
+          f.gslots = sl;
+          const size_t sh = bote::group_smem_bytes(f, n);
+          if (sh <= device_max_lds(p->device) && bote::group_occupancy(n, sh, s->def_obj, f.gbd) >= occ0) break;
+          f.gslots = 0;
+        }
+      }
+      const size_t gshm = bote::group_smem_bytes(f, n);
       if (gshm <= device_max_lds(p->device)) {
         s->group = true;
         s->fshm = gshm;

@@ -46,9 +46,19 @@ constexpr int GROUP_MAX_BD = 1024;
 #ifndef BOTE_GROUP_WAVES
 #define BOTE_GROUP_WAVES 5
 #endif
+// PERM kernels (n <= 7) keep 8 more registers live through the client loop
+// (the byte planes): at <= 96 VGPRs they spill, so they target 4 waves per
+// SIMD (<= 128 VGPRs; measured faster than 5 waves with spills)
+#ifndef BOTE_GROUP_WAVES_PERM
+#define BOTE_GROUP_WAVES_PERM 4
+#endif
 // qtab member planes are 1 << a.gqsh bytes apart (>= gbd * 4, a power of two)
 
 __host__ __device__ constexpr int cmax(int a, int b) { return a > b ? a : b; }
+template <bool B>
+struct BoolC {
+  static constexpr bool value = B;
+};
 
 template <int N>
 struct GCfg {
@@ -58,6 +68,13 @@ struct GCfg {
   // a row's smallest off-diagonal distances that any quorum reads (ranks 0 .. KQ-1)
   static constexpr int KQ = cmax(cmax(QC::qa1, QC::maxf >= 2 ? QC::qa2 : 0), cmax(QC::qe, 3)) - 1;
   static_assert(KQ <= N - 1, "quorum larger than the config");
+  // Register lookup of the members' quorum latencies (n <= 7, two tables):
+  // member m's latency in table t is split into a low and a high byte, kept
+  // in byte m of two 8-byte register planes per table, and a client's value
+  // is picked by v_perm with the nearest member's tag (its index, the low 4
+  // bits of the packed minimum) as the byte selector.  No per-lane LDS
+  // table; larger n gathers from the LDS qtab instead.
+  static constexpr bool PERM = N <= 7 && QC::NL == 2;
 };
 
 // per-wave group line: [mF: cq_quads+1 uint2][Upk: FP*KQ u32][fS1: F u32][fV: F f32]
@@ -66,9 +83,13 @@ __host__ __device__ inline uint32_t gline_bytes(const FastArgs& a, int N, int KQ
   return (a.cq_quads + 1) * 8 + (uint32_t)(FP * KQ + 2 * F) * 4;
 }
 
-__host__ __device__ inline size_t group_layout(const FastArgs& a, int N, int NLW, int KQ, size_t* off) {
+// region 0: PERM kernels: per wave, gslots client lines of (cq_quads + 1)
+// quads; otherwise the qtab (N * NLW member planes of 1 << gqsh bytes)
+__host__ __device__ inline size_t group_layout(const FastArgs& a, int N, int NLW, int KQ, bool perm, size_t* off) {
   size_t o = 0;
-  off[0] = o; o += ((size_t)N * NLW) << a.gqsh;  // qtab first: offsets stay small
+  off[0] = o;
+  o += perm ? (size_t)(a.gbd / 64) * a.gslots * ((a.cq_quads + 1) * 8 + 4) : ((size_t)N * NLW) << a.gqsh;
+  o = (o + 15) & ~(size_t)15;
   off[1] = o; o += (size_t)a.R * (a.cq_quads + 1) * 8;
   off[2] = o; o += a.rq_separate ? (size_t)a.R * (a.rq_quads + 1) * 8 : 0;
   off[3] = o; o += (size_t)a.ns * 4;  // srv
@@ -80,9 +101,9 @@ __host__ __device__ inline size_t group_layout(const FastArgs& a, int N, int NLW
   off[7] = o;  // (binomials stay in global memory: uniform scalar loads, once per group)
   off[8] = o; o += (size_t)(a.gbd / 64) * gline_bytes(a, N, KQ);  // per-wave group lines
   o = (o + 15) & ~(size_t)15;
-  off[9] = o; o += (size_t)a.n_obj * KP * 16;  // top
-  off[10] = o; o += (size_t)64 * 16;          // cand (one wave's candidates)
-  off[11] = o; o += (size_t)KP * 16;          // tmp
+  off[9] = o; o += (size_t)a.n_obj * a.K * 16;  // top: n_obj lists of K records
+  off[10] = o; o += (size_t)64 * 16;           // cand (one wave's candidates)
+  off[11] = o; o += (size_t)a.K * 16;          // tmp
   off[12] = o; o += (size_t)MAXOBJ * 16;      // thr
   off[13] = o; o += 48;                       // lock
   return o;
@@ -91,7 +112,16 @@ __host__ __device__ inline size_t group_layout(const FastArgs& a, int N, int NLW
 template <int N>
 static size_t group_smem_n(const FastArgs& a) {
   size_t off[14];
-  return group_layout(a, N, QCfg<N>::NL <= 2 ? 1 : 2, GCfg<N>::KQ, off);
+  return group_layout(a, N, QCfg<N>::NL <= 2 ? 1 : 2, GCfg<N>::KQ, GCfg<N>::PERM, off);
+}
+
+bool group_uses_lines(uint32_t n) {
+  switch (n) {
+#define PL_CASE(NN) case NN: return GCfg<NN>::PERM;
+    PL_CASE(4) PL_CASE(5) PL_CASE(6) PL_CASE(7)
+#undef PL_CASE
+    default: return false;
+  }
 }
 
 size_t group_smem_bytes(const FastArgs& a, uint32_t n) {
@@ -120,6 +150,9 @@ __device__ __forceinline__ uint2 l64(uint32_t a) {
 __device__ __forceinline__ float lf32(uint32_t a) { return *(const AS3 float*)(uintptr_t)a; }
 __device__ __forceinline__ void s16(uint32_t a, uint32_t v) { *(AS3 uint16_t*)(uintptr_t)a = (uint16_t)v; }
 __device__ __forceinline__ void s32(uint32_t a, uint32_t v) { *(AS3 uint32_t*)(uintptr_t)a = v; }
+__device__ __forceinline__ void s64(uint32_t a, uint32_t lo, uint32_t hi) {
+  *(AS3 uint64_t*)(uintptr_t)a = (uint64_t)lo | ((uint64_t)hi << 32);
+}
 
 __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
@@ -162,10 +195,12 @@ __device__ __forceinline__ void sort_network_pk(uint32_t* a) {
 // ------------------------------------------------ wave-level top-K merge --
 // Called by a whole wavefront (uniform branch).  Takes the block's LDS lock,
 // merges every lane record that beats its objective's K-th record (exact
-// (key, rank) order), updates the thresholds, releases the lock.
+// (key, rank) order), updates the thresholds, releases the lock.  The block
+// lists hold exactly K records each (K <= KP).
 __device__ __forceinline__ void wave_topk(const TopkLds& t, int* lock, int n_obj, uint32_t K,
                                           const uint64_t (&key)[MAXOBJ], const bool (&ok)[MAXOBJ], uint64_t rank) {
   const uint32_t lane = threadIdx.x & 63;
+  const int KL = (int)K;
   if (lane == 0) {
     while (atomicCAS(lock, 0, 1) != 0) __builtin_amdgcn_s_sleep(2);
   }
@@ -174,8 +209,8 @@ __device__ __forceinline__ void wave_topk(const TopkLds& t, int* lock, int n_obj
 #pragma unroll
   for (int o = 0; o < MAXOBJ; ++o) {
     if (o >= n_obj) break;
-    Rec* top = t.top + o * KP;
-    const Rec th = top[K - 1];
+    Rec* top = t.top + o * KL;
+    const Rec th = top[KL - 1];
     const Rec mine = Rec{key[o], rank};
     const bool p = ok[o] && rec_lt(mine, th);
     const uint64_t m = __ballot(p);
@@ -184,22 +219,25 @@ __device__ __forceinline__ void wave_topk(const TopkLds& t, int* lock, int n_obj
     if (p) t.cand[__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0))] = mine;
     wave_sync();
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
+    for (int h = 0; h < KP / 64; ++h) {
       const int e = lane + 64 * h;
-      const Rec x = top[e];
-      int r = e;
-      for (int j = 0; j < n; ++j) r += rec_lt(t.cand[j], x);
-      if (r < KP) t.tmp[r] = x;
+      if (e < KL) {
+        const Rec x = top[e];
+        int r = e;
+        for (int j = 0; j < n; ++j) r += rec_lt(t.cand[j], x);
+        if (r < KL) t.tmp[r] = x;
+      }
     }
     if ((int)lane < n) {
       const Rec y = t.cand[lane];
-      int r = lower_bound_rec(top, KP, y);
+      int r = lower_bound_rec(top, KL, y);
       for (int j = 0; j < n; ++j) r += rec_lt(t.cand[j], y);
-      if (r < KP) t.tmp[r] = y;
+      if (r < KL) t.tmp[r] = y;
     }
     wave_sync();
-    top[lane] = t.tmp[lane];
-    top[lane + 64] = t.tmp[lane + 64];
+#pragma unroll
+    for (int h = 0; h < KP / 64; ++h)
+      if ((int)lane + 64 * h < KL) top[lane + 64 * h] = t.tmp[lane + 64 * h];
     wave_sync();
     if (lane == 0) t.thr[o] = top[K - 1];
     wave_sync();
@@ -227,12 +265,19 @@ __device__ __forceinline__ int cov2_sign(float Vx, uint32_t Sx, float Vy, uint32
   return D < -T ? -1 : (D > T ? 1 : 0);
 }
 
+// u64 -> f32 in three instructions (two conversions and an fma): within
+// 2^-23 relative, inside the screens' error budget
+__device__ __forceinline__ float u64_to_f32(uint64_t x) {
+  return __builtin_fmaf((float)(uint32_t)(x >> 32), 0x1p32f, (float)(uint32_t)x);
+}
+
 // ---------------------------------------------------------- the kernel ----
 // DEF: the default objective set (bote.py DEFAULT_OBJECTIVES: SCORE, MEAN af1,
 // MEAN ff1, COV af1, MEAN e), compiled in; otherwise the objectives come from
 // the arguments (finish_config, bote_fast.hpp).
 template <int N, bool DEF>
-__global__ void __launch_bounds__(GROUP_MAX_BD, BOTE_GROUP_WAVES) sweep_group_kernel(FastArgs a) {
+__global__ void __launch_bounds__(GROUP_MAX_BD, GCfg<N>::PERM ? BOTE_GROUP_WAVES_PERM : BOTE_GROUP_WAVES)
+    sweep_group_kernel(FastArgs a) {
   using QC = QCfg<N>;
   using GC = GCfg<N>;
   constexpr int NL = QC::NL;
@@ -242,15 +287,16 @@ __global__ void __launch_bounds__(GROUP_MAX_BD, BOTE_GROUP_WAVES) sweep_group_ke
   constexpr int KQ = GC::KQ;
   constexpr int PV = Pow2<N - 1>::v;                 // variable row: N-1 values, padded
   constexpr int PF = Pow2<F>::v;                     // fixed-to-fixed row: F values (self = INF), padded
+  constexpr bool PERM = GC::PERM;
   extern __shared__ __align__(16) unsigned char smem[];
   size_t off[14];
-  group_layout(a, N, NLW, KQ, off);
+  group_layout(a, N, NLW, KQ, PERM, off);
   const uint32_t LB = lds_base(smem);
   const uint32_t qtab = LB + (uint32_t)off[0];
   const uint32_t cqt = LB + (uint32_t)off[1];
   const uint32_t rqt = LB + (uint32_t)(a.rq_separate ? off[2] : off[1]);
   uint32_t* srv = (uint32_t*)(smem + off[3]);
-  uint2* lrec = (uint2*)(smem + off[4]);  // per position: .x column sum S1, .y f32 bits of V
+  uint2* lrec = (uint2*)(smem + off[4]);  // per position: .x column sum S1, .y f32 bits of 1 / sqrt(V)
   uint64_t* cs2 = (uint64_t*)(smem + off[5]);
   double* vcol = (double*)(smem + off[6]);
   const uint64_t* binom = a.binom;
@@ -278,7 +324,7 @@ __global__ void __launch_bounds__(GROUP_MAX_BD, BOTE_GROUP_WAVES) sweep_group_ke
     }
   }
   for (uint32_t i = tid; i < a.ns; i += BD) srv[i] = a.srv[i];
-  for (uint32_t i = tid; i < (uint32_t)a.n_obj * KP; i += BD) tk.top[i] = rec_max();
+  for (uint32_t i = tid; i < (uint32_t)a.n_obj * a.K; i += BD) tk.top[i] = rec_max();
   if (tid < MAXOBJ) tk.thr[tid] = rec_max();
   if (tid == 0) *lock = 0;
   __syncthreads();
@@ -295,17 +341,24 @@ __global__ void __launch_bounds__(GROUP_MAX_BD, BOTE_GROUP_WAVES) sweep_group_ke
     cs2[i] = c2;
     const double v = (double)((uint64_t)a.nc * c2 - c1 * c1);  // exact: < 2^53
     vcol[i] = v;
-    lrec[i] = make_uint2((uint32_t)c1, __float_as_uint((float)v));
+    // w = 1 / sqrt(V): a member's COV is sqrt(V) / S, so the leader screen
+    // maximises S * w with no transcendental per config (+inf: COV 0)
+    const float w = v > 0.0 ? (float)(1.0 / sqrt(v)) : __builtin_inff();
+    lrec[i] = make_uint2((uint32_t)c1, __float_as_uint(w));
   }
   __syncthreads();
 
   const uint32_t nc = a.nc, nq = nc >> 2, rem = nc & 3;
   const uint32_t qlane = qtab + tid * 4;
+  // PERM: this wave's client lines (one per distinct (p1, p2) of a step),
+  // then the pairs' keys (lowtab entries)
+  const uint32_t lines = qtab + wid * a.gslots * (cstride + 4);
+  const uint32_t keys = lines + a.gslots * cstride;
   const uint32_t gl = LB + (uint32_t)off[8] + wid * gline_bytes(a, N, KQ);  // this wave's group line
   const uint32_t mfl = gl;                                                 // nearest fixed member per client
   const uint32_t upk = gl + cstride;                                       // packed fixed-row lists
   const uint32_t fS1 = upk + FP * KQ * 4;                                  // fixed column sums
-  const uint32_t fVf = fS1 + F * 4;                                        // fixed column V (f32)
+  const uint32_t fVf = fS1 + F * 4;                                        // fixed column 1 / sqrt(V) (f32)
   const double pnc1 = a.p_fmean * (double)nc, pnc2 = a.p_emean * (double)nc;
   uint64_t valid_cnt = 0, digest = 0;
 
@@ -400,6 +453,50 @@ __global__ void __launch_bounds__(GROUP_MAX_BD, BOTE_GROUP_WAVES) sweep_group_ke
           ok[o] = false;
         }
         const uint64_t rank = r + lane;
+        // ---- PERM: client lines.  Lanes with equal (p1, p2) (consecutive in
+        //      colex order; a lane starts a new pair when p0 == 0) share
+        //      min(member 1, member 2, nearest fixed) per client, built once
+        //      per step, so the client loop merges one lane column into it.
+        //      More distinct pairs than slots: the loop merges all four.
+        uint32_t ll = lines;
+        bool use_lines = false;
+        if constexpr (PERM) {
+          const uint64_t nk = __ballot(have && ((cur & 0xFFu) == 0 || lane == 0));
+          const uint32_t nsl = (uint32_t)__popcll(nk);
+          use_lines = nsl <= a.gslots;
+          if (use_lines) {
+            // slot = index of the lane's pair among the step's pairs; the
+            // first lane of each pair publishes its key to the wave's slot table
+            const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(nk >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)nk, 0));
+            const bool starts = (nk >> lane) & 1;
+            const uint32_t slot = below + (starts ? 1u : 0u) - 1;
+            ll = lines + slot * cstride;
+            if (starts) s32(keys + 4 * slot, cur);
+            wave_sync();
+            // then lpl lanes per line (one quad = 4 clients each), 64 / lpl
+            // lines per pass
+            const uint32_t nqq = nq + (rem ? 1u : 0u);
+            const uint32_t lsh = nqq <= 16 ? 4u : (nqq <= 32 ? 5u : 6u), lpl = 1u << lsh;
+            const uint32_t li = lane >> lsh, qx = lane & (lpl - 1);
+            for (uint32_t sl = 0; sl < nsl; sl += 64u >> lsh) {
+              const uint32_t sx = sl + li;
+              if (sx < nsl) {
+                const uint32_t k = l32(keys + 4 * sx);
+                const uint32_t p1 = (k >> 8) & 0xFFu, p2 = k >> 16;
+                const uint32_t b1 = cqt + (a.srv_identity ? p1 : srv[p1]) * cstride;
+                const uint32_t b2 = cqt + (a.srv_identity ? p2 : srv[p2]) * cstride;
+                const uint32_t dst = lines + sx * cstride;
+                for (uint32_t x = qx; x < nqq; x += lpl) {
+                  const uint2 v1 = l64(b1 + 8 * x), v2 = l64(b2 + 8 * x), vf = l64(mfl + 8 * x);
+                  const us2 lo = pk_min(pk_min(as_us2(v1.x | 0x00010001u), as_us2(v2.x | 0x00020002u)), as_us2(vf.x));
+                  const us2 hi = pk_min(pk_min(as_us2(v1.y | 0x00010001u), as_us2(v2.y | 0x00020002u)), as_us2(vf.y));
+                  s64(dst + 8 * x, as_u32(lo), as_u32(hi));
+                }
+              }
+            }
+            wave_sync();
+          }
+        }
         if (have) {
           uint32_t pv[3], rv[3];
           pv[0] = cur & 0xFF;
@@ -416,9 +513,25 @@ __global__ void __launch_bounds__(GROUP_MAX_BD, BOTE_GROUP_WAVES) sweep_group_ke
           uint32_t cS2[NL];
 #pragma unroll
           for (int t = 0; t < NL; ++t) cS2[t] = 0;
+          // PERM: each table's member latencies as packed pair words, index
+          // 0: members (0, 1), 1: member 2, 2 + pp: fixed members (3 + 2pp, 4 + 2pp)
+          uint32_t wp[2][2 + FP];
           // sorted row (packed pair: lo = member j, hi = member j + 1)
           auto emit_pk = [&](int j, bool has_hi, const uint32_t* L) {
             const uint32_t w0 = L[QC::lq(0) - 2], w1 = L[(NL >= 2 ? QC::lq(1) : QC::lq(0)) - 2];
+            if constexpr (PERM) {
+              Q2[j] = L[0] & 0xFFFFu;
+              Q3[j] = L[1] & 0xFFFFu;
+              if (has_hi) {
+                Q2[j + 1] = L[0] >> 16;
+                Q3[j + 1] = L[1] >> 16;
+              }
+              const int pi = j == 0 ? 0 : (j == 2 ? 1 : 2 + (j - 3) / 2);
+              const uint32_t hm = has_hi ? ~0u : 0xFFFFu;
+              wp[0][pi] = w0 & hm;
+              wp[1][pi] = w1 & hm;
+              return;
+            }
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
               if (h == 1 && !has_hi) break;
@@ -427,7 +540,7 @@ __global__ void __launch_bounds__(GROUP_MAX_BD, BOTE_GROUP_WAVES) sweep_group_ke
               Q2[j + h] = (L[0] >> sh) & 0xFFFFu;
               Q3[j + h] = (L[1] >> sh) & 0xFFFFu;
               const uint32_t word = NL >= 2 ? __builtin_amdgcn_perm(w1, w0, sel) : ((w0 >> sh) & 0xFFFFu);
-              s32(qlane + ((uint32_t)(j + h) << qsh), word);
+              if (!ABLATE(a, 1024)) s32(qlane + ((uint32_t)(j + h) << qsh), word);
               cS1p += word;
               const uint32_t q0 = word & 0xFFFFu;
               cS2[0] += q0 * q0;
@@ -503,6 +616,10 @@ __global__ void __launch_bounds__(GROUP_MAX_BD, BOTE_GROUP_WAVES) sweep_group_ke
 #pragma unroll
             for (int k = 0; k < KQ; ++k) {
               us2 z = A[k];
+              if (ABLATE(a, 64)) {
+                L[k] = as_u32(pk_min(z, y[k < 3 ? k : 2]));
+                continue;
+              }
 #pragma unroll
               for (int j = 1; j <= 3 && j <= k + 1; ++j) {
                 const int i = k + 1 - j;  // elements taken from A
@@ -512,48 +629,68 @@ __global__ void __launch_bounds__(GROUP_MAX_BD, BOTE_GROUP_WAVES) sweep_group_ke
             }
             emit_pk(3 + 2 * pp, has_hi, L);
           }
+          // ---- PERM: byte planes (member m's latency: low byte in byte m of
+          //      QL, high byte in byte m of QH; members 0..3 in .x, 4..6 in
+          //      .y) and the colocated sums over the members
+          uint2 QL[2], QH[2];
+          if constexpr (PERM) {
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+              const uint32_t w01 = wp[t][0], w2 = wp[t][1], w34 = wp[t][2], w56 = FP >= 2 ? wp[t][FP >= 2 ? 3 : 2] : 0u;
+              QL[t].x = __builtin_amdgcn_perm(w2, w01, 0x0C040200u) | (w34 << 24);
+              QH[t].x = __builtin_amdgcn_perm(w34, __builtin_amdgcn_perm(w2, w01, 0x0C050301u), 0x05020100u);
+              QL[t].y = __builtin_amdgcn_perm(w56, w34, 0x0C060402u);
+              QH[t].y = __builtin_amdgcn_perm(w56, w34, 0x0C070503u);
+              uint32_t ps = 0, sq = 0;
+#pragma unroll
+              for (int i = 0; i < 2 + FP; ++i) {
+                ps += wp[t][i];
+                sq = __builtin_amdgcn_udot2(as_us2(wp[t][i]), as_us2(wp[t][i]), sq, false);
+              }
+              cS2[t] = sq;
+              cS1p |= ((ps & 0xFFFFu) + (ps >> 16)) << (16 * t);
+            }
+          }
           // ---- FPaxos leader (f = 1, q = 2, min COV, first in config order)
           auto pos_of = [&](int l) { return l < 3 ? pv[l] : hq[l - 3]; };
           auto reg_of = [&](int l) { return l < 3 ? rv[l] : freg[l - 3]; };
-          uint2 vrec[3];  // the variable members' (S1, f32 V): one 8-byte LDS read each
+          uint2 vrec[3];  // the variable members' (S1, f32 1 / sqrt(V)): one 8-byte LDS read each
 #pragma unroll
           for (int i = 0; i < 3; ++i) vrec[i] = lrec[pv[i]];
           auto s1_of = [&](int l) { return l < 3 ? vrec[l].x : l32(fS1 + 4 * (l - 3)); };
-          auto vf_of = [&](int l) { return l < 3 ? __uint_as_float(vrec[l].y) : lf32(fVf + 4 * (l - 3)); };
-          // COV^2 proxy r = V / S^2 per member in f32 (V one rounding, S
-          // exact below 2^24, S^2 and the reciprocal one each): within 2^-22
+          auto wf_of = [&](int l) { return l < 3 ? __uint_as_float(vrec[l].y) : lf32(fVf + 4 * (l - 3)); };
+          auto vf_of = [&](int l) { return (float)vcol[pos_of(l)]; };  // (exact re-scan only)
+          // 1 / COV proxy t = S / sqrt(V) = S * w per member in f32 (S exact
+          // below 2^24, w and the product one rounding each): within 2^-23
           // of exact, so comparisons outside a 2^-18 band are decided; any
           // closer call re-runs the scan exactly (cov2_sign) or defers.
-          // Decided without a sequential scan: m = min r (a tree), the
+          // Decided without a sequential scan: m = max t (a tree), the
           // leader is the first member at m, and the decision is ambiguous
-          // when m > 0 and another member lies within the 2^-18 band above m
-          // (exact zeros, V = 0, tie exactly and keep the first, as the
-          // reference's first-minimum does).
+          // when m is finite and another member lies within the 2^-18 band
+          // below m (exact zeros, V = 0, t = inf, tie exactly and keep the
+          // first, as the reference's first-minimum does).
           uint32_t bi = 0;
           bool amb = false;
           if (!ABLATE(a, 128)) {
-            float rl[N];
+            float tl[N];
 #pragma unroll
-            for (int l = 0; l < N; ++l) {
-              const float fs = (float)(s1_of(l) + __umul24(nc, Q2[l]));
-              rl[l] = vf_of(l) * __builtin_amdgcn_rcpf(fs * fs);
-            }
-            float mn[N];
+            for (int l = 0; l < N; ++l) tl[l] = (float)(s1_of(l) + __umul24(nc, Q2[l])) * wf_of(l);
+            float mx[N];
 #pragma unroll
-            for (int l = 0; l < N; ++l) mn[l] = rl[l];
+            for (int l = 0; l < N; ++l) mx[l] = tl[l];
 #pragma unroll
             for (int w = 1; w < N; w <<= 1)
 #pragma unroll
-              for (int l = 0; l + w < N; l += 2 * w) mn[l] = fminf(mn[l], mn[l + w]);
-            const float m = mn[0], lim = m * (1.0f + 0x1p-18f);
+              for (int l = 0; l + w < N; l += 2 * w) mx[l] = fmaxf(mx[l], mx[l + w]);
+            const float m = mx[0], lim = m * (1.0f - 0x1p-18f);
             uint32_t eq = 0, nearm = 0;
 #pragma unroll
             for (int l = 0; l < N; ++l) {
-              eq |= (rl[l] == m ? 1u : 0u) << l;
-              nearm |= (rl[l] <= lim ? 1u : 0u) << l;
+              eq |= (tl[l] == m ? 1u : 0u) << l;
+              nearm |= (tl[l] >= lim ? 1u : 0u) << l;
             }
             bi = (uint32_t)__builtin_ctz(eq);
-            amb = m > 0.0f && __builtin_popcount(nearm) > 1;
+            amb = m < __builtin_inff() && __builtin_popcount(nearm) > 1;
           }
           if (amb) {  // exact re-scan in the generic path's arithmetic
             amb = false;
@@ -615,16 +752,25 @@ __global__ void __launch_bounds__(GROUP_MAX_BD, BOTE_GROUP_WAVES) sweep_group_ke
                 asm("v_lshl_add_u32 %0, %1, %2, %3" : "=v"(r) : "v"(m), "s"(qsh), "v"(qlane));
                 return r;
               };
-              auto quad = [&](uint32_t g8, uint32_t mlo, uint32_t mhi) {
-                const uint2 wa = l64(c0 + g8), wb = l64(c1 + g8), wc = l64(c2 + g8), wf = l64(mfl + g8);
-                const us2 lo = pk_min(pk_min(as_us2(wa.x), as_us2(wb.x) | J1), pk_min(as_us2(wc.x) | J2, as_us2(wf.x)));
-                const us2 hi = pk_min(pk_min(as_us2(wa.y), as_us2(wb.y) | J1), pk_min(as_us2(wc.y) | J2, as_us2(wf.y)));
+              // each client's nearest member, packed (latency << 4 | member):
+              // the lane's member-0 column against its client line, or
+              // against the other three sources when no line was built
+              auto nearest = [&](auto lines_c, uint32_t g8, us2& lo, us2& hi) {
+                const uint2 wa = l64(c0 + g8);
+                if constexpr (decltype(lines_c)::value) {
+                  const uint2 wl = l64(ll + g8);
+                  lo = pk_min(as_us2(wa.x), as_us2(wl.x));
+                  hi = pk_min(as_us2(wa.y), as_us2(wl.y));
+                } else {
+                  const uint2 wb = l64(c1 + g8), wc = l64(c2 + g8), wf = l64(mfl + g8);
+                  lo = pk_min(pk_min(as_us2(wa.x), as_us2(wb.x) | J1), pk_min(as_us2(wc.x) | J2, as_us2(wf.x)));
+                  hi = pk_min(pk_min(as_us2(wa.y), as_us2(wb.y) | J1), pk_min(as_us2(wc.y) | J2, as_us2(wf.y)));
+                }
+              };
+              auto quad = [&](auto lines_c, uint32_t g8, uint32_t mlo, uint32_t mhi) {
+                us2 lo, hi;
+                nearest(lines_c, g8, lo, hi);
                 const uint32_t L = as_u32(lo), H = as_u32(hi);
-                // qtab address of each client's nearest member: one bitfield
-                // extract + one v_lshl_add per client; the two tables are the
-                // halves of the member's word, read straight into packed pairs
-                const uint32_t a0 = qaddr(L & 15u), a1 = qaddr(__builtin_amdgcn_ubfe(L, 16, 4));
-                const uint32_t a2 = qaddr(H & 15u), a3 = qaddr(__builtin_amdgcn_ubfe(H, 16, 4));
                 const us2 dlo = lo >> (us2)4, dhi = hi >> (us2)4;
                 auto acc1 = [&](int t, us2 q01, us2 q23) {
                   // packed adds as one 32-bit add: no carry crosses the halves
@@ -634,18 +780,37 @@ __global__ void __launch_bounds__(GROUP_MAX_BD, BOTE_GROUP_WAVES) sweep_group_ke
                   s2[t] = __builtin_amdgcn_udot2(as_us2(a01), as_us2(a01), s2[t], false);
                   s2[t] = __builtin_amdgcn_udot2(as_us2(a23), as_us2(a23), s2[t], false);
                 };
-                // (16-bit loads into packed halves would need d16 loads, which
-                //  gfx950 with sramecc does not preserve; read words and perm)
-                const uint32_t w0 = l32(a0), w1 = l32(a1), w2 = l32(a2), w3 = l32(a3);
-                acc1(0, as_us2(__builtin_amdgcn_perm(w1, w0, 0x05040100u)), as_us2(__builtin_amdgcn_perm(w3, w2, 0x05040100u)));
-                if (NL >= 2)
-                  acc1(NL >= 2 ? 1 : 0, as_us2(__builtin_amdgcn_perm(w1, w0, 0x07060302u)),
-                       as_us2(__builtin_amdgcn_perm(w3, w2, 0x07060302u)));
-                if (NL == 3) {
-                  const uint32_t P2 = (uint32_t)N << qsh;
-                  const uint32_t x0 = l32(a0 + P2), x1 = l32(a1 + P2), x2 = l32(a2 + P2), x3 = l32(a3 + P2);
-                  acc1(NL - 1, as_us2(__builtin_amdgcn_perm(x1, x0, 0x05040100u)),
-                       as_us2(__builtin_amdgcn_perm(x3, x2, 0x05040100u)));
+                if constexpr (PERM) {
+                  // the 4 clients' member tags as byte selectors, then per
+                  // table the low and high bytes of their members' latencies
+                  // (v_perm over the byte planes), interleaved into u16 pairs
+                  const uint32_t sel = __builtin_amdgcn_perm(H, L, 0x06040200u) & 0x0F0F0F0Fu;
+#pragma unroll
+                  for (int t = 0; t < 2; ++t) {
+                    const uint32_t bl = __builtin_amdgcn_perm(QL[t].y, QL[t].x, sel);
+                    const uint32_t bh = __builtin_amdgcn_perm(QH[t].y, QH[t].x, sel);
+                    acc1(t, as_us2(__builtin_amdgcn_perm(bh, bl, 0x05010400u)),
+                         as_us2(__builtin_amdgcn_perm(bh, bl, 0x07030602u)));
+                  }
+                } else {
+                  // qtab address of each client's nearest member: one bitfield
+                  // extract + one v_lshl_add per client; the two tables are the
+                  // halves of the member's word, read straight into packed pairs
+                  const uint32_t a0 = qaddr(L & 15u), a1 = qaddr(__builtin_amdgcn_ubfe(L, 16, 4));
+                  const uint32_t a2 = qaddr(H & 15u), a3 = qaddr(__builtin_amdgcn_ubfe(H, 16, 4));
+                  // (16-bit loads into packed halves would need d16 loads, which
+                  //  gfx950 with sramecc does not preserve; read words and perm)
+                  const uint32_t w0 = l32(a0), w1 = l32(a1), w2 = l32(a2), w3 = l32(a3);
+                  acc1(0, as_us2(__builtin_amdgcn_perm(w1, w0, 0x05040100u)), as_us2(__builtin_amdgcn_perm(w3, w2, 0x05040100u)));
+                  if (NL >= 2)
+                    acc1(NL >= 2 ? 1 : 0, as_us2(__builtin_amdgcn_perm(w1, w0, 0x07060302u)),
+                         as_us2(__builtin_amdgcn_perm(w3, w2, 0x07060302u)));
+                  if (NL == 3) {
+                    const uint32_t P2 = (uint32_t)N << qsh;
+                    const uint32_t x0 = l32(a0 + P2), x1 = l32(a1 + P2), x2 = l32(a2 + P2), x3 = l32(a3 + P2);
+                    acc1(NL - 1, as_us2(__builtin_amdgcn_perm(x1, x0, 0x05040100u)),
+                         as_us2(__builtin_amdgcn_perm(x3, x2, 0x05040100u)));
+                  }
                 }
               };
               auto flush = [&]() {
@@ -660,15 +825,15 @@ __global__ void __launch_bounds__(GROUP_MAX_BD, BOTE_GROUP_WAVES) sweep_group_ke
               const uint32_t nql = ABLATE(a, 1) ? 0u : nq;
               // 4 quads per iteration (constant offsets fold into the ds_read
               // offset fields); s2 is flushed to 64 bits every s2_flush quads
-              {
+              auto clients = [&](auto lines_c) {
                 const uint32_t f4 = a.g_flush >> 2 ? a.g_flush >> 2 : 1u;
                 uint32_t g = 0, k = 0;
                 if (a.g_flush >= 4) {
                   for (; g + 4 <= nql; g += 4) {
-                    quad(g * 8, ~0u, ~0u);
-                    quad(g * 8 + 8, ~0u, ~0u);
-                    quad(g * 8 + 16, ~0u, ~0u);
-                    quad(g * 8 + 24, ~0u, ~0u);
+                    quad(lines_c, g * 8, ~0u, ~0u);
+                    quad(lines_c, g * 8 + 8, ~0u, ~0u);
+                    quad(lines_c, g * 8 + 16, ~0u, ~0u);
+                    quad(lines_c, g * 8 + 24, ~0u, ~0u);
                     if (++k == f4) {
                       flush();
                       k = 0;
@@ -678,14 +843,16 @@ __global__ void __launch_bounds__(GROUP_MAX_BD, BOTE_GROUP_WAVES) sweep_group_ke
                 }
                 for (uint32_t g0 = g; g0 < nql; g0 += a.g_flush) {
                   const uint32_t ge = min(nql, g0 + a.g_flush);
-                  for (g = g0; g < ge; ++g) quad(g * 8, ~0u, ~0u);
+                  for (g = g0; g < ge; ++g) quad(lines_c, g * 8, ~0u, ~0u);
                   flush();
                 }
-              }
-              if (rem && !ABLATE(a, 1)) {
-                quad(nq * 8, rem >= 2 ? ~0u : 0x0000FFFFu, rem == 3 ? 0x0000FFFFu : 0u);
-                flush();
-              }
+                if (rem && !ABLATE(a, 1)) {
+                  quad(lines_c, nq * 8, rem >= 2 ? ~0u : 0x0000FFFFu, rem == 3 ? 0x0000FFFFu : 0u);
+                  flush();
+                }
+              };
+              if (PERM && use_lines) clients(BoolC<PERM>{});
+              else clients(BoolC<false>{});
               if (ABLATE(a, 1)) {  // timing only: non-degenerate dummy sums
 #pragma unroll
                 for (int t = 0; t < NL; ++t) {
@@ -726,7 +893,7 @@ __global__ void __launch_bounds__(GROUP_MAX_BD, BOTE_GROUP_WAVES) sweep_group_ke
             }
             const double vlead = vcol[lpos];
             const float vlead32 = (float)vlead;
-            float r_af1 = -1.0f;  // af1's V / S^2 when the validity scan computed it
+            float v_af1 = -1.0f;  // af1's V (f32) when the validity scan computed it
             if (DEF) {
               // ---- compute_score validity (search.rs:421-472), exact
               bool valid = false;
@@ -749,14 +916,11 @@ __global__ void __launch_bounds__(GROUP_MAX_BD, BOTE_GROUP_WAVES) sweep_group_ke
                     // cov_f >= cov_a (min_fairness_fpaxos_improv == 0 on this path)
                     const uint64_t Va = mom_v(ma);
                     if (!(vlead == 0.0 && Va == 0)) {
-                      const float sf = (float)(uint32_t)mf.s1, sa = (float)(uint32_t)ma.s1;
-                      const float rf = vlead32 * __builtin_amdgcn_rcpf(sf * sf);
-                      const float ra = (float)Va * __builtin_amdgcn_rcpf(sa * sa);
-                      if (f == 1) r_af1 = ra;
-                      int c = rf > ra * (1.0f + 0x1p-18f) ? 1 : (rf < ra * (1.0f - 0x1p-18f) ? -1 : 0);
-                      if (c == 0)
-                        c = cov2_sign(vlead32, (uint32_t)mf.s1, (float)Va, (uint32_t)ma.s1, [&] { return vlead; },
-                                      [&] { return (double)Va; });
+                      // cross-multiplied f32 screen, then f64 (cov2_sign)
+                      const float vaf = u64_to_f32(Va);
+                      if (f == 1) v_af1 = vaf;
+                      const int c = cov2_sign(vlead32, (uint32_t)mf.s1, vaf, (uint32_t)ma.s1, [&] { return vlead; },
+                                              [&] { return (double)Va; });
                       if (c == 0) defer = true;
                       valid = valid && c > 0;
                     }
@@ -781,6 +945,7 @@ __global__ void __launch_bounds__(GROUP_MAX_BD, BOTE_GROUP_WAVES) sweep_group_ke
                   digest += digest_final(rank, bi, h);
                 }
                 // ---- default objectives: 0 SCORE, 1 MEAN af1, 2 MEAN ff1, 3 COV af1, 4 MEAN e
+                if (ABLATE(a, 2048)) valid = false;
                 ok[1] = ok[2] = ok[4] = true;
                 key[1] = mom[SLOT_AF1].s1;
                 key[2] = mom[SLOT_FF1].s1;
@@ -824,12 +989,10 @@ __global__ void __launch_bounds__(GROUP_MAX_BD, BOTE_GROUP_WAVES) sweep_group_ke
                   // f32 screen with a 2^-10 margin (conservative: offers a superset)
                   bool maybe = tk3 == ~0ull;
                   if (!maybe) {
-                    float r = r_af1;
-                    if (r < 0.0f) {
-                      const float S = (float)(uint32_t)m.s1;
-                      r = (float)mom_v(m) * __builtin_amdgcn_rcpf(S * S);
-                    }
-                    maybe = r <= (float)__longlong_as_double((long long)tk3) * (1.0f + 0x1p-10f);
+                    // V / S^2 <= threshold, cross-multiplied
+                    const float S = (float)(uint32_t)m.s1;
+                    const float V = v_af1 >= 0.0f ? v_af1 : u64_to_f32(mom_v(m));
+                    maybe = V <= (float)__longlong_as_double((long long)tk3) * (S * S) * (1.0f + 0x1p-10f);
                   }
                   if (maybe) {
                     ok[3] = true;
@@ -881,7 +1044,10 @@ __global__ void __launch_bounds__(GROUP_MAX_BD, BOTE_GROUP_WAVES) sweep_group_ke
   if (digest) atomicAdd(&a.out_counters[1], (unsigned long long)digest);
   __syncthreads();
   Rec* dst = a.out_top + (size_t)blockIdx.x * a.n_obj * KP;
-  for (uint32_t i = tid; i < (uint32_t)a.n_obj * KP; i += BD) dst[i] = tk.top[i];
+  for (uint32_t i = tid; i < (uint32_t)a.n_obj * KP; i += BD) {
+    const uint32_t o = i / KP, e = i % KP;
+    dst[i] = e < a.K ? tk.top[o * a.K + e] : rec_max();
+  }
 }
 
 // ------------------------------------------------------------- launcher ---

@@ -92,6 +92,7 @@ struct FastArgs {
   uint32_t g_flush;   // group kernel: quads per flush of its 32-bit square sums and packed-u16 sums
   uint32_t gbd;       // group kernel: workgroup size (multiple of 64, <= 1024)
   uint32_t gqsh;      // group kernel: log2 of the qtab plane stride in bytes (1 << gqsh >= gbd * 4)
+  uint32_t gslots;    // group kernel, n <= 7: client lines per wave (0: none), see bote_group.hip
   int want_score, p_int;
   int64_t p1i, p2i;  // p_int: min_mean_{fpaxos,epaxos}_improv * nc as integers
   double p_fmean, p_emean;
@@ -128,6 +129,7 @@ size_t fast_smem_bytes(const FastArgs& a, uint32_t n);
 int fast_occupancy(uint32_t n, size_t shm);
 hipError_t launch_fast(const FastArgs& a, uint32_t n, uint32_t grid, size_t shm, hipStream_t st);
 size_t group_smem_bytes(const FastArgs& a, uint32_t n);
+bool group_uses_lines(uint32_t n);  // n <= 7: client lines (FastArgs::gslots) and register lookups
 int group_occupancy(uint32_t n, size_t shm, bool def_objectives, uint32_t bd);
 hipError_t launch_group(const FastArgs& a, uint32_t n, bool def_objectives, uint32_t grid, size_t shm, hipStream_t st);
 
