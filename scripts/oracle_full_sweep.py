@@ -12,9 +12,13 @@ and bench.py's result check compare the device sweep against it.
 
   python scripts/oracle_full_sweep.py --workload r64n7 --threads 6
 
-The per-chunk results go to oracle/build/<name>_chunks.jsonl, so a killed run
-resumes where it stopped.  Ranges: --rank-begin/--rank-end restrict the sweep
-(window fixtures, e.g. R=128 n=6).
+The per-chunk results go to oracle/build/<name>_chunks.jsonl (or --state), so a
+killed run resumes where it stopped.  Ranges: --rank-begin/--rank-end restrict
+the sweep (window fixtures, e.g. R=128 n=6).  Splitting one sweep over hosts:
+--partial with --sweep-begin (a chunk-aligned rank inside the range) and
+--time-limit sweeps chunks from there and only appends them to the state file;
+concatenating the state files and re-running without --partial writes the
+fixture (chunks already present are not recomputed).
 """
 import argparse
 import json
@@ -60,6 +64,10 @@ def main():
     ap.add_argument("--rank-begin", type=int, default=0)
     ap.add_argument("--rank-end", type=int, default=None)
     ap.add_argument("--name", default=None)
+    ap.add_argument("--state", default=None, help="chunk state file (default oracle/build/<name>_chunks.jsonl)")
+    ap.add_argument("--partial", action="store_true", help="sweep chunks only; write no fixture")
+    ap.add_argument("--sweep-begin", type=int, default=None, help="first chunk to sweep (chunk-aligned)")
+    ap.add_argument("--time-limit", type=float, default=None, help="stop after this many seconds")
     args = ap.parse_args()
 
     R, n = WORKLOADS[args.workload]
@@ -69,24 +77,32 @@ def main():
     re = total if args.rank_end is None else args.rank_end
     name = args.name or (f"syn_{args.workload}_full" if (rb, re) == (0, total) else
                          f"syn_{args.workload}_{rb}_{re}")
-    state = os.path.join(ROOT, "oracle", "build", f"{name}_chunks.jsonl")
+    state = args.state or os.path.join(ROOT, "oracle", "build", f"{name}_chunks.jsonl")
     os.makedirs(os.path.dirname(state), exist_ok=True)
     done = {}
     if os.path.exists(state):
         for line in open(state):
             line = line.strip()
             if line:
-                d = json.loads(line)
+                try:
+                    d = json.loads(line)
+                except ValueError:  # a line cut short by a killed run
+                    continue
                 done[d["begin"]] = d
     o = O.OraclePlanet.of(planet)
     srv = np.arange(R, dtype=np.uint32)
     t_start = time.time()
     swept = 0
+    sb = rb if args.sweep_begin is None else args.sweep_begin
+    assert (sb - rb) % args.chunk == 0, "--sweep-begin must be chunk-aligned"
     with open(state, "a") as fh:
-        for b in range(rb, re, args.chunk):
+        for b in range(sb, re, args.chunk):
             e = min(re, b + args.chunk)
             if b in done:
                 continue
+            if args.time_limit is not None and time.time() - t_start > args.time_limit:
+                print(f"[{name}] time limit reached at rank {b}", flush=True)
+                break
             t0 = time.time()
             tops, valid, digest = o.sweep(srv, srv, n, b, e, OBJECTIVES, args.K, RPARAMS, FT_F1F2, args.threads)
             d = {"begin": b, "end": e, "valid": valid, "digest": digest,
@@ -99,6 +115,8 @@ def main():
             left = sum(min(re, x + args.chunk) - x for x in range(rb, re, args.chunk) if x not in done)
             print(f"[{name}] {e - rb}/{re - rb} ranks; {swept / el:.0f} configs/s; ~{left / max(swept / el, 1):.0f} s left",
                   flush=True)
+    if args.partial:
+        return
     parts = [done[b] for b in sorted(done) if rb <= b < re]
     covered = sum(p["end"] - p["begin"] for p in parts)
     assert covered == re - rb, (covered, re - rb)
