@@ -75,12 +75,24 @@ struct GCfg {
   // bits of the packed minimum) as the byte selector.  No per-lane LDS
   // table; larger n gathers from the LDS qtab instead.
   static constexpr bool PERM = N <= 7 && QC::NL == 2;
+  // Per-position table (n <= 7, at most 4 fixed members): for every position
+  // x below the group's smallest fixed position, 16 bytes computed once per
+  // group: x's distances to the fixed members, sorted (row part), and the
+  // fixed members' distances to x, packed in the fixed-row pairs (column
+  // part).  A lane's three variable rows then start from their sorted fixed
+  // parts and merge in the two distances to the other variable members, and
+  // the fixed rows' inserts come packed: 3 LDS reads instead of 24 u16 reads
+  // and two full row sorts.
+  static constexpr bool RX = N <= 7;
+  static_assert(!RX || (F <= 4 && KQ <= 4), "position table holds 4 fixed members");
 };
 
-// per-wave group line: [mF: cq_quads+1 uint2][Upk: FP*KQ u32][fS1: F u32][fV: F f32]
+// per-wave group line: [rx: ns x 16 B (n <= 7)][mF: cq_quads+1 uint2][Upk: FP*KQ u32][fS1: F u32][fV: F f32],
+// padded to 16 bytes
+__host__ __device__ inline uint32_t gline_rx_bytes(const FastArgs& a, int N) { return N <= 7 ? a.ns * 16 : 0u; }
 __host__ __device__ inline uint32_t gline_bytes(const FastArgs& a, int N, int KQ) {
   const int F = N - 3, FP = (F + 1) / 2;
-  return (a.cq_quads + 1) * 8 + (uint32_t)(FP * KQ + 2 * F) * 4;
+  return (gline_rx_bytes(a, N) + (a.cq_quads + 1) * 8 + (uint32_t)(FP * KQ + 2 * F) * 4 + 15) & ~15u;
 }
 
 // region 0: PERM kernels: per wave, gslots client lines of (cq_quads + 1)
@@ -99,6 +111,7 @@ __host__ __device__ inline size_t group_layout(const FastArgs& a, int N, int NLW
   off[5] = o; o += (size_t)a.ns * 8;                   // cs2
   off[6] = o; o += (size_t)a.ns * 8;                   // vcol (f64)
   off[7] = o;  // (binomials stay in global memory: uniform scalar loads, once per group)
+  o = (o + 15) & ~(size_t)15;
   off[8] = o; o += (size_t)(a.gbd / 64) * gline_bytes(a, N, KQ);  // per-wave group lines
   o = (o + 15) & ~(size_t)15;
   off[9] = o; o += (size_t)a.n_obj * a.K * 16;  // top: n_obj lists of K records
@@ -147,11 +160,24 @@ __device__ __forceinline__ uint2 l64(uint32_t a) {
   const uint64_t v = *(const AS3 uint64_t*)(uintptr_t)a;
   return make_uint2((uint32_t)v, (uint32_t)(v >> 32));
 }
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 l128(uint32_t a) {
+  const u32x4 v = *(const AS3 u32x4*)(uintptr_t)a;
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
 __device__ __forceinline__ float lf32(uint32_t a) { return *(const AS3 float*)(uintptr_t)a; }
 __device__ __forceinline__ void s16(uint32_t a, uint32_t v) { *(AS3 uint16_t*)(uintptr_t)a = (uint16_t)v; }
 __device__ __forceinline__ void s32(uint32_t a, uint32_t v) { *(AS3 uint32_t*)(uintptr_t)a = v; }
 __device__ __forceinline__ void s64(uint32_t a, uint32_t lo, uint32_t hi) {
   *(AS3 uint64_t*)(uintptr_t)a = (uint64_t)lo | ((uint64_t)hi << 32);
+}
+__device__ __forceinline__ void s128(uint32_t a, uint4 v) {
+  u32x4 w;
+  w.x = v.x;
+  w.y = v.y;
+  w.z = v.z;
+  w.w = v.w;
+  *(AS3 u32x4*)(uintptr_t)a = w;
 }
 
 __device__ __forceinline__ void wave_sync() {
@@ -189,6 +215,28 @@ __device__ __forceinline__ void sort_network_pk(uint32_t* a) {
         }
       }
     }
+  }
+}
+
+// The KO smallest of the union of two ascending lists A (KA entries) and y
+// (KY entries), ascending: the k-th is the min over the splits (k+1-j from A,
+// j from y) of max(A[k-j], y[j-1]).  T: u32 (min/max) or us2 (two lists at
+// once, packed halves).
+template <int KA, int KY, int KO, class T>
+__device__ __forceinline__ void merge_lists(const T* A, const T* y, T* L) {
+#pragma unroll
+  for (int k = 0; k < KO; ++k) {
+    T z = k < KA ? A[k < KA ? k : 0] : y[0];
+    bool have = k < KA;
+#pragma unroll
+    for (int j = 1; j <= KY && j <= k + 1; ++j) {
+      const int i = k + 1 - j;  // elements taken from A
+      if (i > KA) continue;
+      const T c = i == 0 ? y[j - 1] : __builtin_elementwise_max(A[i > 0 ? i - 1 : 0], y[j - 1]);
+      z = have ? __builtin_elementwise_min(z, c) : c;
+      have = true;
+    }
+    L[k] = z;
   }
 }
 
@@ -355,8 +403,9 @@ __global__ void __launch_bounds__(GROUP_MAX_BD, GCfg<N>::PERM ? BOTE_GROUP_WAVES
   const uint32_t lines = qtab + wid * a.gslots * (cstride + 4);
   const uint32_t keys = lines + a.gslots * cstride;
   const uint32_t gl = LB + (uint32_t)off[8] + wid * gline_bytes(a, N, KQ);  // this wave's group line
-  const uint32_t mfl = gl;                                                 // nearest fixed member per client
-  const uint32_t upk = gl + cstride;                                       // packed fixed-row lists
+  const uint32_t rxt = gl;                                                 // per-position table (RX)
+  const uint32_t mfl = gl + gline_rx_bytes(a, N);                          // nearest fixed member per client
+  const uint32_t upk = mfl + cstride;                                      // packed fixed-row lists
   const uint32_t fS1 = upk + FP * KQ * 4;                                  // fixed column sums
   const uint32_t fVf = fS1 + F * 4;                                        // fixed column 1 / sqrt(V) (f32)
   const double pnc1 = a.p_fmean * (double)nc, pnc2 = a.p_emean * (double)nc;
@@ -431,6 +480,24 @@ __global__ void __launch_bounds__(GROUP_MAX_BD, GCfg<N>::PERM ? BOTE_GROUP_WAVES
           for (int k = 0; k < F; ++k) key = min(key, l16(cqt + freg[k] * cstride + 2 * c) | (uint32_t)(3 + k));
         }
         s16(mfl + 2 * c, key);
+      }
+      if constexpr (GC::RX) {
+        // positions below the smallest fixed one: sorted distances to the
+        // fixed members (row part), the fixed members' distances to x
+        // (column part, packed as the fixed-row pairs); absent members INF
+        for (uint32_t x = lane; x < hq[0]; x += 64) {
+          const uint32_t rg = a.srv_identity ? x : srv[x];
+          uint32_t rf[4], cf[4];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const uint32_t fk = freg[k < F ? k : 0];
+            rf[k] = k < F ? l16(rqt + fk * rstride + 2 * rg) >> LAT_SHIFT : 0xFFFFu;
+            cf[k] = k < F ? l16(rqt + rg * rstride + 2 * fk) >> LAT_SHIFT : 0xFFFFu;
+          }
+          sort_network<4>(rf);
+          s128(rxt + 16 * x, make_uint4(rf[0] | (rf[1] << 16), rf[2] | (rf[3] << 16), cf[0] | (cf[1] << 16),
+                                        cf[2] | (cf[3] << 16)));
+        }
       }
       wave_sync();
 
@@ -556,78 +623,144 @@ __global__ void __launch_bounds__(GROUP_MAX_BD, GCfg<N>::PERM ? BOTE_GROUP_WAVES
               }
             }
           };
-          // ---- Q phase, variable rows 0 and 1 (packed), row 2 (lo half)
-          {
-            uint32_t v[PV];
-            // (stored latencies are << 4, so one shift of the packed pair is exact)
-            v[0] = (l16(cv[1] + 2 * rv[0]) | (l16(cv[0] + 2 * rv[1]) << 16)) >> LAT_SHIFT;  // d(0,1) | d(1,0)
-            v[1] = (l16(cv[2] + 2 * rv[0]) | (l16(cv[2] + 2 * rv[1]) << 16)) >> LAT_SHIFT;  // d(0,2) | d(1,2)
+          if constexpr (GC::RX) {
+            // ---- Q phase from the group's position table: each variable
+            //      row = its sorted fixed part + the 2 distances to the other
+            //      variable members; each fixed row = the group's sorted
+            //      fixed-to-fixed list + the lane's 3 distances (packed)
+            const uint4 X0 = l128(rxt + 16 * pv[0]), X1 = l128(rxt + 16 * pv[1]), X2 = l128(rxt + 16 * pv[2]);
+            {  // rows 0 and 1, packed (lo: member 0, hi: member 1)
+              us2 A[4], y[2], L[KQ];
+              A[0] = as_us2(__builtin_amdgcn_perm(X1.x, X0.x, 0x05040100u));
+              A[1] = as_us2(__builtin_amdgcn_perm(X1.x, X0.x, 0x07060302u));
+              A[2] = as_us2(__builtin_amdgcn_perm(X1.y, X0.y, 0x05040100u));
+              A[3] = as_us2(__builtin_amdgcn_perm(X1.y, X0.y, 0x07060302u));
+              // (stored latencies are << 4, so one shift of the packed pair is exact)
+              y[0] = as_us2((l16(cv[1] + 2 * rv[0]) | (l16(cv[0] + 2 * rv[1]) << 16)) >> LAT_SHIFT);  // d(0,1) | d(1,0)
+              y[1] = as_us2((l16(cv[2] + 2 * rv[0]) | (l16(cv[2] + 2 * rv[1]) << 16)) >> LAT_SHIFT);  // d(0,2) | d(1,2)
+              const us2 t = pk_min(y[0], y[1]);
+              y[1] = pk_max(y[0], y[1]);
+              y[0] = t;
+              merge_lists<F < 4 ? F : 4, 2, KQ>(A, y, L);
+              uint32_t W[KQ];
 #pragma unroll
-            for (int k = 0; k < F; ++k) {
-              const uint32_t fc = rqt + freg[k] * rstride;
-              v[2 + k] = (l16(fc + 2 * rv[0]) | (l16(fc + 2 * rv[1]) << 16)) >> LAT_SHIFT;
+              for (int k = 0; k < KQ; ++k) W[k] = as_u32(L[k]);
+              emit_pk(0, true, W);
+            }
+            {  // row 2
+              uint32_t A[4], y[2], L[KQ];
+              A[0] = X2.x & 0xFFFFu;
+              A[1] = X2.x >> 16;
+              A[2] = X2.y & 0xFFFFu;
+              A[3] = X2.y >> 16;
+              const uint32_t d20 = l16(cv[0] + 2 * rv[2]) >> LAT_SHIFT, d21 = l16(cv[1] + 2 * rv[2]) >> LAT_SHIFT;
+              y[0] = min(d20, d21);
+              y[1] = max(d20, d21);
+              merge_lists<F < 4 ? F : 4, 2, KQ>(A, y, L);
+              emit_pk(2, false, L);
             }
 #pragma unroll
-            for (int k = N - 1; k < PV; ++k) v[k] = 0xFFFFFFFFu;
-            if (!ABLATE(a, 32)) sort_network_pk<PV>(v);
-            emit_pk(0, true, v);
-          }
-          {
-            uint32_t v[PV];
-            v[0] = l16(cv[0] + 2 * rv[2]) >> LAT_SHIFT;
-            v[1] = l16(cv[1] + 2 * rv[2]) >> LAT_SHIFT;
+            for (int pp = 0; pp < FP; ++pp) {
+              us2 A[KQ];  // the group's sorted fixed-row lists (uniform)
 #pragma unroll
-            for (int k = 0; k < F; ++k) v[2 + k] = l16(rqt + freg[k] * rstride + 2 * rv[2]) >> LAT_SHIFT;
+              for (int i = 0; i < KQ; ++i) A[i] = as_us2(l32(upk + (pp * KQ + i) * 4));
+              const bool has_hi = 2 * pp + 1 < F;
+              us2 y[3];  // the 3 lane distances (d(f, m) | d(f', m)), sorted
+              y[0] = as_us2(pp == 0 ? X0.z : X0.w);
+              y[1] = as_us2(pp == 0 ? X1.z : X1.w);
+              y[2] = as_us2(pp == 0 ? X2.z : X2.w);
+              {
+                us2 t = pk_min(y[0], y[1]);
+                y[1] = pk_max(y[0], y[1]);
+                y[0] = t;
+                t = pk_min(y[1], y[2]);
+                y[2] = pk_max(y[1], y[2]);
+                y[1] = t;
+                t = pk_min(y[0], y[1]);
+                y[1] = pk_max(y[0], y[1]);
+                y[0] = t;
+              }
+              us2 L[KQ];
+              merge_lists<KQ, 3, KQ>(A, y, L);
+              uint32_t W[KQ];
 #pragma unroll
-            for (int k = N - 1; k < PV; ++k) v[k] = 0xFFFFu;
-            if (!ABLATE(a, 32)) sort_network<PV>(v);
-            emit_pk(2, false, v);
-          }
-          // ---- fixed rows (pairs): insert the 3 lane distances into the
-          //      group's packed sorted lists
-#pragma unroll
-          for (int pp = 0; pp < FP; ++pp) {
-            us2 A[KQ];  // the group's sorted fixed-row lists (uniform)
-#pragma unroll
-            for (int i = 0; i < KQ; ++i) A[i] = as_us2(l32(upk + (pp * KQ + i) * 4));
-            const bool has_hi = 2 * pp + 1 < F;
-            us2 y[3];  // the 3 lane distances, then sorted (3 compare-exchanges)
-#pragma unroll
-            for (int m = 0; m < 3; ++m) {
-              const uint32_t lo = l16(cv[m] + 2 * freg[2 * pp]);
-              const uint32_t hi = has_hi ? l16(cv[m] + 2 * freg[has_hi ? 2 * pp + 1 : 2 * pp]) : 0xFFF0u;
-              y[m] = as_us2((lo | (hi << 16)) >> LAT_SHIFT);
-              if (!has_hi) y[m] = as_us2(as_u32(y[m]) | 0xFFFF0000u);
+              for (int k = 0; k < KQ; ++k) W[k] = as_u32(L[k]);
+              emit_pk(3 + 2 * pp, has_hi, W);
+            }
+          } else {
+            // ---- Q phase, variable rows 0 and 1 (packed), row 2 (lo half)
+            {
+              uint32_t v[PV];
+              // (stored latencies are << 4, so one shift of the packed pair is exact)
+              v[0] = (l16(cv[1] + 2 * rv[0]) | (l16(cv[0] + 2 * rv[1]) << 16)) >> LAT_SHIFT;  // d(0,1) | d(1,0)
+              v[1] = (l16(cv[2] + 2 * rv[0]) | (l16(cv[2] + 2 * rv[1]) << 16)) >> LAT_SHIFT;  // d(0,2) | d(1,2)
+  #pragma unroll
+              for (int k = 0; k < F; ++k) {
+                const uint32_t fc = rqt + freg[k] * rstride;
+                v[2 + k] = (l16(fc + 2 * rv[0]) | (l16(fc + 2 * rv[1]) << 16)) >> LAT_SHIFT;
+              }
+  #pragma unroll
+              for (int k = N - 1; k < PV; ++k) v[k] = 0xFFFFFFFFu;
+              if (!ABLATE(a, 32)) sort_network_pk<PV>(v);
+              emit_pk(0, true, v);
             }
             {
-              us2 t = pk_min(y[0], y[1]);
-              y[1] = pk_max(y[0], y[1]);
-              y[0] = t;
-              t = pk_min(y[1], y[2]);
-              y[2] = pk_max(y[1], y[2]);
-              y[1] = t;
-              t = pk_min(y[0], y[1]);
-              y[1] = pk_max(y[0], y[1]);
-              y[0] = t;
+              uint32_t v[PV];
+              v[0] = l16(cv[0] + 2 * rv[2]) >> LAT_SHIFT;
+              v[1] = l16(cv[1] + 2 * rv[2]) >> LAT_SHIFT;
+  #pragma unroll
+              for (int k = 0; k < F; ++k) v[2 + k] = l16(rqt + freg[k] * rstride + 2 * rv[2]) >> LAT_SHIFT;
+  #pragma unroll
+              for (int k = N - 1; k < PV; ++k) v[k] = 0xFFFFu;
+              if (!ABLATE(a, 32)) sort_network<PV>(v);
+              emit_pk(2, false, v);
             }
-            // merge: the k-th smallest of A u y is the min over the splits
-            // (k+1-j from A, j from y) of max(A[k-j], y[j-1])
-            uint32_t L[KQ];
-#pragma unroll
-            for (int k = 0; k < KQ; ++k) {
-              us2 z = A[k];
-              if (ABLATE(a, 64)) {
-                L[k] = as_u32(pk_min(z, y[k < 3 ? k : 2]));
-                continue;
+            // ---- fixed rows (pairs): insert the 3 lane distances into the
+            //      group's packed sorted lists
+  #pragma unroll
+            for (int pp = 0; pp < FP; ++pp) {
+              us2 A[KQ];  // the group's sorted fixed-row lists (uniform)
+  #pragma unroll
+              for (int i = 0; i < KQ; ++i) A[i] = as_us2(l32(upk + (pp * KQ + i) * 4));
+              const bool has_hi = 2 * pp + 1 < F;
+              us2 y[3];  // the 3 lane distances, then sorted (3 compare-exchanges)
+  #pragma unroll
+              for (int m = 0; m < 3; ++m) {
+                const uint32_t lo = l16(cv[m] + 2 * freg[2 * pp]);
+                const uint32_t hi = has_hi ? l16(cv[m] + 2 * freg[has_hi ? 2 * pp + 1 : 2 * pp]) : 0xFFF0u;
+                y[m] = as_us2((lo | (hi << 16)) >> LAT_SHIFT);
+                if (!has_hi) y[m] = as_us2(as_u32(y[m]) | 0xFFFF0000u);
               }
-#pragma unroll
-              for (int j = 1; j <= 3 && j <= k + 1; ++j) {
-                const int i = k + 1 - j;  // elements taken from A
-                z = pk_min(z, i == 0 ? y[j - 1] : pk_max(A[i > 0 ? i - 1 : 0], y[j - 1]));
+              {
+                us2 t = pk_min(y[0], y[1]);
+                y[1] = pk_max(y[0], y[1]);
+                y[0] = t;
+                t = pk_min(y[1], y[2]);
+                y[2] = pk_max(y[1], y[2]);
+                y[1] = t;
+                t = pk_min(y[0], y[1]);
+                y[1] = pk_max(y[0], y[1]);
+                y[0] = t;
               }
-              L[k] = as_u32(z);
+              // merge: the k-th smallest of A u y is the min over the splits
+              // (k+1-j from A, j from y) of max(A[k-j], y[j-1])
+              uint32_t L[KQ];
+  #pragma unroll
+              for (int k = 0; k < KQ; ++k) {
+                us2 z = A[k];
+                if (ABLATE(a, 64)) {
+                  L[k] = as_u32(pk_min(z, y[k < 3 ? k : 2]));
+                  continue;
+                }
+  #pragma unroll
+                for (int j = 1; j <= 3 && j <= k + 1; ++j) {
+                  const int i = k + 1 - j;  // elements taken from A
+                  z = pk_min(z, i == 0 ? y[j - 1] : pk_max(A[i > 0 ? i - 1 : 0], y[j - 1]));
+                }
+                L[k] = as_u32(z);
+              }
+              emit_pk(3 + 2 * pp, has_hi, L);
             }
-            emit_pk(3 + 2 * pp, has_hi, L);
           }
           // ---- PERM: byte planes (member m's latency: low byte in byte m of
           //      QL, high byte in byte m of QH; members 0..3 in .x, 4..6 in
