@@ -67,6 +67,7 @@ def main():
     ap.add_argument("--state", default=None, help="chunk state file (default oracle/build/<name>_chunks.jsonl)")
     ap.add_argument("--partial", action="store_true", help="sweep chunks only; write no fixture")
     ap.add_argument("--sweep-begin", type=int, default=None, help="first chunk to sweep (chunk-aligned)")
+    ap.add_argument("--sweep-end", type=int, default=None, help="stop before this rank (with --partial)")
     ap.add_argument("--time-limit", type=float, default=None, help="stop after this many seconds")
     args = ap.parse_args()
 
@@ -96,7 +97,7 @@ def main():
     sb = rb if args.sweep_begin is None else args.sweep_begin
     assert (sb - rb) % args.chunk == 0, "--sweep-begin must be chunk-aligned"
     with open(state, "a") as fh:
-        for b in range(sb, re, args.chunk):
+        for b in range(sb, re if args.sweep_end is None else min(re, args.sweep_end), args.chunk):
             e = min(re, b + args.chunk)
             if b in done:
                 continue

@@ -65,3 +65,20 @@ def test_oracle_topk_matches_fixture(topk, case):
                                   RP, 2, 4)
     assert valid == c["valid"] and str(digest) == c["digest"]
     assert [[[str(k), r] for k, r in t] for t in tops] == c["tops"]
+
+
+def test_full_r64n7_fixture_keys_rederived():
+    """tests/golden/syn_r64n7_full.json (the oracle over all 621,216,192 ranks,
+    scripts/oracle_full_sweep.py): every list is sorted by (key, rank) and the
+    first 20 records of each objective carry the key the oracle computes for
+    that single config."""
+    fx = json.load(open(os.path.join(G, "syn_r64n7_full.json")))
+    assert (fx["R"], fx["n"], fx["rank_begin"], fx["rank_end"]) == (64, 7, 0, comb(64, 7))
+    p = Planet.synthetic(64)
+    o = O.OraclePlanet.of(p)
+    s = np.arange(64, dtype=np.uint32)
+    for oi, t in enumerate(fx["tops"]):
+        assert len(t) == fx["K"] and t == sorted(t)
+        for key, rank in t[:20]:
+            tops, _, _ = o.sweep(s, s, 7, rank, rank + 1, DEFAULT_OBJECTIVES, 1, RP, 2, 1)
+            assert tops[oi] == [(key, rank)], (oi, rank)
