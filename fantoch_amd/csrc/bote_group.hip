@@ -808,22 +808,17 @@ __global__ void __launch_bounds__(GROUP_MAX_BD, GCfg<N>::PERM ? BOTE_GROUP_WAVES
             float tl[N];
 #pragma unroll
             for (int l = 0; l < N; ++l) tl[l] = (float)(s1_of(l) + __umul24(nc, Q2[l])) * wf_of(l);
-            float mx[N];
+            // the largest and second largest (with multiplicity) t: a
+            // running max and median-of-three, 2 ops per member
+            float m = tl[0], m2 = -1.0f;
 #pragma unroll
-            for (int l = 0; l < N; ++l) mx[l] = tl[l];
-#pragma unroll
-            for (int w = 1; w < N; w <<= 1)
-#pragma unroll
-              for (int l = 0; l + w < N; l += 2 * w) mx[l] = fmaxf(mx[l], mx[l + w]);
-            const float m = mx[0], lim = m * (1.0f - 0x1p-18f);
-            uint32_t eq = 0, nearm = 0;
-#pragma unroll
-            for (int l = 0; l < N; ++l) {
-              eq |= (tl[l] == m ? 1u : 0u) << l;
-              nearm |= (tl[l] >= lim ? 1u : 0u) << l;
+            for (int l = 1; l < N; ++l) {
+              m2 = __builtin_amdgcn_fmed3f(m, m2, tl[l]);
+              m = fmaxf(m, tl[l]);
             }
-            bi = (uint32_t)__builtin_ctz(eq);
-            amb = m < __builtin_inff() && __builtin_popcount(nearm) > 1;
+#pragma unroll
+            for (int l = N - 1; l >= 0; --l) bi = tl[l] == m ? (uint32_t)l : bi;  // the first at m
+            amb = m < __builtin_inff() && m2 >= m * (1.0f - 0x1p-18f);
           }
           if (amb) {  // exact re-scan in the generic path's arithmetic
             amb = false;
@@ -1026,9 +1021,19 @@ __global__ void __launch_bounds__(GROUP_MAX_BD, GCfg<N>::PERM ? BOTE_GROUP_WAVES
             }
             const double vlead = vcol[lpos];
             const float vlead32 = (float)vlead;
-            float v_af1 = -1.0f;  // af1's V (f32) when the validity scan computed it
+            // af1's exact V (leaderless sums S1 < 2^21, so one 32x32 square),
+            // shared by the validity test and the COV-af1 objective screen
+            auto mom_v32 = [](const Mom& m) {
+              const uint32_t s1 = (uint32_t)m.s1;
+              return (uint64_t)m.cnt * m.s2 - (uint64_t)s1 * s1;
+            };
+            const uint64_t Va1 = mom_v32(mom[SLOT_AF1]);
+            const float va1 = u64_to_f32(Va1);
             if (DEF) {
-              // ---- compute_score validity (search.rs:421-472), exact
+              // ---- compute_score validity (search.rs:421-472), exact.  The
+              //      integer mean tests of every f first; the COV tests only
+              //      for configs that pass them, and a config is deferred
+              //      only when its validity hinges on an ambiguous COV call.
               bool valid = false;
               const int fcap = min(N / 2, a.ft_metric);
               bool defer = false;
@@ -1040,31 +1045,38 @@ __global__ void __launch_bounds__(GROUP_MAX_BD, GCfg<N>::PERM ? BOTE_GROUP_WAVES
                   const Mom& ma = mom[f == 1 ? SLOT_AF1 : SLOT_AF2];
                   const Mom& mf = mom[f == 1 ? SLOT_FF1 : SLOT_FF2];
                   // fmi >= p1: integers unless the sums meet exactly
-                  const int64_t D = (int64_t)mf.s1 - (int64_t)ma.s1;
+                  const int32_t D = (int32_t)((uint32_t)mf.s1 - (uint32_t)ma.s1);
                   bool mok;
-                  if (a.p_int && D != a.p1i) mok = D > a.p1i;
+                  if (a.p_int && (int64_t)D != a.p1i) mok = (int64_t)D > a.p1i;
                   else mok = (mom_mean(mf) - mom_mean(ma)) >= a.p_fmean;
                   valid = valid && mok;
-                  if (valid) {
-                    // cov_f >= cov_a (min_fairness_fpaxos_improv == 0 on this path)
-                    const uint64_t Va = mom_v(ma);
-                    if (!(vlead == 0.0 && Va == 0)) {
-                      // cross-multiplied f32 screen, then f64 (cov2_sign)
-                      const float vaf = u64_to_f32(Va);
-                      if (f == 1) v_af1 = vaf;
-                      const int c = cov2_sign(vlead32, (uint32_t)mf.s1, vaf, (uint32_t)ma.s1, [&] { return vlead; },
-                                              [&] { return (double)Va; });
-                      if (c == 0) defer = true;
-                      valid = valid && c > 0;
-                    }
-                  }
                   if (N == 11 || N == 13) {
-                    const int64_t De = (int64_t)mom[SLOT_E].s1 - (int64_t)ma.s1;
+                    const int32_t De = (int32_t)((uint32_t)mom[SLOT_E].s1 - (uint32_t)ma.s1);
                     bool eok;
-                    if (a.p_int && De != a.p2i) eok = De > a.p2i;
+                    if (a.p_int && (int64_t)De != a.p2i) eok = (int64_t)De > a.p2i;
                     else eok = (mom_mean(mom[SLOT_E]) - mom_mean(ma)) >= a.p_emean;
                     valid = valid && eok;
                   }
+                }
+                if (valid) {
+                  // cov_f >= cov_a (min_fairness_fpaxos_improv == 0 on this path):
+                  // cross-multiplied f32 screen, then f64 (cov2_sign)
+                  bool lt = false, amb_c = false;
+#pragma unroll
+                  for (int f = 1; f <= 2; ++f) {
+                    if (f > fcap) break;
+                    const Mom& ma = mom[f == 1 ? SLOT_AF1 : SLOT_AF2];
+                    const Mom& mf = mom[f == 1 ? SLOT_FF1 : SLOT_FF2];
+                    const uint64_t Va = f == 1 ? Va1 : mom_v32(ma);
+                    if (vlead == 0.0 && Va == 0) continue;  // both COV 0
+                    const float vaf = f == 1 ? va1 : u64_to_f32(Va);
+                    const int c = cov2_sign(vlead32, (uint32_t)mf.s1, vaf, (uint32_t)ma.s1, [&] { return vlead; },
+                                            [&] { return (double)Va; });
+                    lt = lt || c < 0;
+                    amb_c = amb_c || c == 0;
+                  }
+                  valid = !lt && !amb_c;
+                  defer = !lt && amb_c;
                 }
               }
               if (defer) {
@@ -1124,8 +1136,7 @@ __global__ void __launch_bounds__(GROUP_MAX_BD, GCfg<N>::PERM ? BOTE_GROUP_WAVES
                   if (!maybe) {
                     // V / S^2 <= threshold, cross-multiplied
                     const float S = (float)(uint32_t)m.s1;
-                    const float V = v_af1 >= 0.0f ? v_af1 : u64_to_f32(mom_v(m));
-                    maybe = V <= (float)__longlong_as_double((long long)tk3) * (S * S) * (1.0f + 0x1p-10f);
+                    maybe = va1 <= (float)__longlong_as_double((long long)tk3) * (S * S) * (1.0f + 0x1p-10f);
                   }
                   if (maybe) {
                     ok[3] = true;
