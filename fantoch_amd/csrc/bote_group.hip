@@ -641,7 +641,12 @@ __global__ void __launch_bounds__(GROUP_MAX_BD, GCfg<N>::PERM ? BOTE_GROUP_WAVES
               const us2 t = pk_min(y[0], y[1]);
               y[1] = pk_max(y[0], y[1]);
               y[0] = t;
-              merge_lists<F < 4 ? F : 4, 2, KQ>(A, y, L);
+              if (ABLATE(a, 32)) {
+#pragma unroll
+                for (int k = 0; k < KQ; ++k) L[k] = pk_min(A[k], y[k & 1]);
+              } else {
+                merge_lists<F < 4 ? F : 4, 2, KQ>(A, y, L);
+              }
               uint32_t W[KQ];
 #pragma unroll
               for (int k = 0; k < KQ; ++k) W[k] = as_u32(L[k]);
@@ -681,7 +686,12 @@ __global__ void __launch_bounds__(GROUP_MAX_BD, GCfg<N>::PERM ? BOTE_GROUP_WAVES
                 y[0] = t;
               }
               us2 L[KQ];
-              merge_lists<KQ, 3, KQ>(A, y, L);
+              if (ABLATE(a, 64)) {
+#pragma unroll
+                for (int k = 0; k < KQ; ++k) L[k] = pk_min(A[k], y[k < 3 ? k : 2]);
+              } else {
+                merge_lists<KQ, 3, KQ>(A, y, L);
+              }
               uint32_t W[KQ];
 #pragma unroll
               for (int k = 0; k < KQ; ++k) W[k] = as_u32(L[k]);
