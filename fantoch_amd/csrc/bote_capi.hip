@@ -801,6 +801,7 @@ int bote_sweep_create_ex(const bote_planet* p, const uint32_t* servers, uint32_t
       f.gbd = bote::FAST_BD;
       f.gqsh = 10;
       f.gslots = 0;
+      f.grx = 0;
       // bote.py DEFAULT_OBJECTIVES: SCORE, MEAN af1, MEAN ff1, COV af1, MEAN e
       static const uint32_t dk[5] = {BOTE_OBJ_SCORE, BOTE_OBJ_MEAN, BOTE_OBJ_MEAN, BOTE_OBJ_COV, BOTE_OBJ_MEAN};
       static const uint32_t ds[5] = {0, BOTE_SLOT_AF1, BOTE_SLOT_FF1, BOTE_SLOT_AF1, BOTE_SLOT_E};
@@ -808,6 +809,12 @@ int bote_sweep_create_ex(const bote_planet* p, const uint32_t* servers, uint32_t
       for (uint32_t o = 0; s->def_obj && o < 5; ++o)
         s->def_obj = objs[o].kind == dk[o] && (dk[o] == BOTE_OBJ_SCORE || objs[o].slot == ds[o]);
       if (bote::group_uses_lines(n)) {
+        // the per-group position table (n <= 7) unless its LDS lowers the
+        // workgroups per CU (R = 64: 4 either way, register-bound; R = 128:
+        // 3 without, 2 with it, measured 255 vs 280 ms)
+        const int occ_plain = bote::group_occupancy(n, bote::group_smem_bytes(f, n), s->def_obj, f.gbd);
+        f.grx = 1;
+        if (bote::group_occupancy(n, bote::group_smem_bytes(f, n), s->def_obj, f.gbd) < occ_plain) f.grx = 0;
         // client lines per wave: as many (<= 16) as keep the workgroups per
         // CU of the kernel without lines (a step has 7.7 distinct (p1, p2)
         // on average at R=64 n=7, 4.0 at R=128 n=6)

@@ -83,13 +83,16 @@ struct GCfg {
   // parts and merge in the two distances to the other variable members, and
   // the fixed rows' inserts come packed: 3 LDS reads instead of 24 u16 reads
   // and two full row sorts.
+  // (a launch argument, FastArgs::grx: the table costs ns x 16 B of LDS per
+  // wave, which at R = 128 lowers the workgroups per CU, so the host enables
+  // it only where the occupancy stays)
   static constexpr bool RX = N <= 7;
   static_assert(!RX || (F <= 4 && KQ <= 4), "position table holds 4 fixed members");
 };
 
 // per-wave group line: [rx: ns x 16 B (n <= 7)][mF: cq_quads+1 uint2][Upk: FP*KQ u32][fS1: F u32][fV: F f32],
 // padded to 16 bytes
-__host__ __device__ inline uint32_t gline_rx_bytes(const FastArgs& a, int N) { return N <= 7 ? a.ns * 16 : 0u; }
+__host__ __device__ inline uint32_t gline_rx_bytes(const FastArgs& a, int N) { return N <= 7 && a.grx ? a.ns * 16 : 0u; }
 __host__ __device__ inline uint32_t gline_bytes(const FastArgs& a, int N, int KQ) {
   const int F = N - 3, FP = (F + 1) / 2;
   return (gline_rx_bytes(a, N) + (a.cq_quads + 1) * 8 + (uint32_t)(FP * KQ + 2 * F) * 4 + 15) & ~15u;
@@ -481,7 +484,7 @@ __global__ void __launch_bounds__(GROUP_MAX_BD, GCfg<N>::PERM ? BOTE_GROUP_WAVES
         }
         s16(mfl + 2 * c, key);
       }
-      if constexpr (GC::RX) {
+      if (GC::RX && a.grx) {
         // positions below the smallest fixed one: sorted distances to the
         // fixed members (row part), the fixed members' distances to x
         // (column part, packed as the fixed-row pairs); absent members INF
@@ -623,7 +626,7 @@ __global__ void __launch_bounds__(GROUP_MAX_BD, GCfg<N>::PERM ? BOTE_GROUP_WAVES
               }
             }
           };
-          if constexpr (GC::RX) {
+          if (GC::RX && a.grx) {
             // ---- Q phase from the group's position table: each variable
             //      row = its sorted fixed part + the 2 distances to the other
             //      variable members; each fixed row = the group's sorted
