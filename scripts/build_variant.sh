@@ -11,7 +11,15 @@ H="/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=
 for f in bote_kernels bote_sweep bote_group bote_quorums bote_chain bote_capi; do
   src=fantoch_amd/csrc/$f.hip
   if [ "$f" = bote_group ] && [ -n "${GROUP_SRC:-}" ]; then src=$GROUP_SRC; fi
-  if [ "$f" = bote_group ] || [ ! -f $D/obj/$f.o ]; then $H -I fantoch_amd/csrc -c $src -o $D/obj/$f.o & fi
+  # rebuild when the object is missing or older than its source or any shared
+  # header (a stale object with an old FastArgs layout faults on the device)
+  stale=0
+  [ "$f" = bote_group ] && stale=1
+  [ -f $D/obj/$f.o ] || stale=1
+  for dep in $src fantoch_amd/csrc/*.hpp include/bote_hip.h; do
+    [ -f $D/obj/$f.o ] && [ "$dep" -nt $D/obj/$f.o ] && stale=1
+  done
+  if [ $stale = 1 ]; then $H -I fantoch_amd/csrc -c $src -o $D/obj/$f.o & fi
 done
 wait
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $D/libbote_hip.so $D/obj/*.o
