@@ -10,6 +10,8 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <map>
+#include <memory>
 #include <vector>
 
 #include "../../include/bote_hip.h"
@@ -149,6 +151,15 @@ struct bote_sweep {
   size_t fshm = 0;
   uint32_t xgrid = 0;  // generic fixup grid (deferred configs)
   DBuf cqt, rqt, queue, qcount, lowtab;
+  // group kernel work chunks per launch range (cached: a bench or a shard
+  // re-launches the same range), plus the ticket counter
+  struct Chunks {
+    std::vector<uint64_t> host;  // kept alive: the async upload reads it
+    DBuf dev;
+    uint32_t n = 0;
+  };
+  std::map<std::pair<uint64_t, uint64_t>, std::unique_ptr<Chunks>> chunks;
+  DBuf wctr;
   uint64_t last_rb = 0, last_re = 0;
   hipStream_t last_stream = nullptr;
   uint64_t result_bytes() const { return (uint64_t)n_obj * bote::KP * 16 + 16; }
@@ -196,6 +207,70 @@ double group_utilisation(uint32_t ns, uint32_t n) {
     steps += groups * (long double)((g + 63) / 64);
   }
   return steps > 0 ? (double)(cfg / (64 * steps)) : 0.0;
+}
+
+// Cost-balanced work chunks of [rb, re) for the group kernel
+// (FastArgs::wchunks).  Groups are walked in rank order: a group of C(q0, 3)
+// configs (q0 = its smallest fixed position) contributes ceil(part / 64)
+// wavefront steps plus GROUP_COST steps of per-group precompute for the part
+// of it inside the range.  Returns nchunks + 1 boundaries, or nothing when the
+// range has too many groups to walk (the kernel then splits ranks evenly).
+constexpr double GROUP_COST = 1.5;
+constexpr uint64_t MAX_WALK_GROUPS = 40000000;
+std::vector<uint64_t> group_chunks(uint32_t ns, uint32_t n, uint64_t rb, uint64_t re, uint32_t nchunks) {
+  std::vector<uint64_t> out;
+  if (re <= rb || n < 4 || nchunks == 0) return out;
+  const uint32_t F = n - 3;
+  // colex unrank of rb: p[j] = the largest m with C(m, j + 1) <= rest
+  std::vector<uint32_t> p(n);
+  uint64_t rest = rb;
+  uint32_t hi = ns;
+  for (int j = (int)n - 1; j >= 0; --j) {
+    uint32_t m = (uint32_t)j;
+    while (m + 1 < hi && binom_u64(m + 1, j + 1) <= rest) ++m;
+    p[j] = m;
+    rest -= binom_u64(m, j + 1);
+    hi = m;
+  }
+  std::vector<uint32_t> q(p.begin() + 3, p.end());
+  std::vector<uint64_t> gb, gl;  // group parts inside the range: start, length
+  std::vector<double> gc;
+  double total = 0;
+  for (;;) {
+    uint64_t base = 0;
+    for (uint32_t k = 0; k < F; ++k) base += binom_u64(q[k], k + 4);
+    const uint64_t g = binom_u64(q[0], 3);
+    const uint64_t b = std::max(base, rb), e = std::min(base + g, re);
+    if (b >= re) break;
+    if (e > b) {
+      const double c = (double)((e - b + 63) / 64) + GROUP_COST;
+      gb.push_back(b);
+      gl.push_back(e - b);
+      gc.push_back(c);
+      total += c;
+      if (gb.size() > MAX_WALK_GROUPS) return out;
+    }
+    if (e >= re) break;
+    // colex successor of the fixed positions (a combination of {3 .. ns-1})
+    uint32_t k = 0;
+    while (k < F && q[k] + 1 >= (k + 1 < F ? q[k + 1] : ns)) ++k;
+    if (k == F) break;
+    ++q[k];
+    for (uint32_t j = 0; j < k; ++j) q[j] = 3 + j;
+  }
+  out.reserve(nchunks + 1);
+  out.push_back(rb);
+  double cum = 0;
+  size_t i = 0;
+  for (uint32_t c = 1; c < nchunks; ++c) {
+    const double tgt = total * c / nchunks;
+    while (i < gc.size() && cum + gc[i] <= tgt) cum += gc[i++];
+    uint64_t bnd = re;
+    if (i < gc.size()) bnd = gb[i] + (uint64_t)((tgt - cum) / gc[i] * (double)gl[i]);
+    out.push_back(std::max(out.back(), std::min(bnd, re)));
+  }
+  out.push_back(re);
+  return out;
 }
 
 // Packed (p0 | p1 << 8 | p2 << 16) 3-subsets of [0, m) in colex order.
@@ -939,6 +1014,34 @@ static int launch_fast_path(bote_sweep* s, uint64_t rb, uint64_t re, hipStream_t
   f.runlen = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(32, count / (G * 8)));
   HIP_TRY(hipMemsetAsync(s->counters.p, 0, 16, st));
   HIP_TRY(hipMemsetAsync(s->qcount.p, 0, 8, st));
+  if (s->group) {
+    // cost-balanced chunks, 4 per wave, taken dynamically (bote_group.hip)
+    auto key = std::make_pair(rb, re);
+    auto it = s->chunks.find(key);
+    if (it == s->chunks.end()) {
+      if (s->chunks.size() >= 16) {  // bounded cache: drain the last stream before freeing
+        if (s->last_stream) HIP_TRY(hipStreamSynchronize(s->last_stream));
+        HIP_TRY(hipStreamSynchronize(st));
+        s->chunks.clear();
+      }
+      auto c = std::make_unique<bote_sweep::Chunks>();
+      const uint32_t nwaves = s->fgrid * (f.gbd / 64);
+      c->host = group_chunks(s->ns, s->n, rb, re, nwaves * 4);
+      if (!c->host.empty()) {
+        c->n = (uint32_t)c->host.size() - 1;
+        if (c->dev.alloc(c->host.size() * 8) != hipSuccess) return fail(BOTE_E_NOMEM, "hipMalloc work chunks");
+        HIP_TRY(hipMemcpyAsync(c->dev.p, c->host.data(), c->host.size() * 8, hipMemcpyHostToDevice, st));
+      }
+      it = s->chunks.emplace(key, std::move(c)).first;
+    }
+    f.nwchunks = it->second->n;
+    f.wchunks = it->second->dev.as<uint64_t>();
+    if (f.nwchunks) {
+      if (!s->wctr.p && s->wctr.alloc(16) != hipSuccess) return fail(BOTE_E_NOMEM, "hipMalloc work counter");
+      f.wctr = s->wctr.as<unsigned int>();
+      HIP_TRY(hipMemsetAsync(s->wctr.p, 0, 4, st));
+    }
+  }
   hipEvent_t *e0 = nullptr, *e1 = nullptr;
   int rc;
   if ((rc = timing_slot(s, e0, e1))) return rc;

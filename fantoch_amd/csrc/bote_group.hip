@@ -414,12 +414,30 @@ __global__ void __launch_bounds__(GROUP_MAX_BD, GCfg<N>::PERM ? BOTE_GROUP_WAVES
   const double pnc1 = a.p_fmean * (double)nc, pnc2 = a.p_emean * (double)nc;
   uint64_t valid_cnt = 0, digest = 0;
 
-  // this wave's contiguous share of [rb, re)
-  const uint64_t nwaves = (uint64_t)gridDim.x * WPB;
-  const uint64_t gw = (uint64_t)blockIdx.x * WPB + wid;
-  const uint64_t total = a.re - a.rb;
-  uint64_t r = uni64(a.rb + (uint64_t)(((unsigned __int128)total * gw) / nwaves));
-  const uint64_t rend = uni64(a.rb + (uint64_t)(((unsigned __int128)total * (gw + 1)) / nwaves));
+  // Work: either this wave's equal share of [rb, re), or (nwchunks > 0)
+  // chunks of equal estimated cost taken from a ticket counter until none is
+  // left.  Rank shares of equal size are not equal work: a group of C(p3, 3)
+  // configs costs ceil(C(p3, 3) / 64) steps plus its precompute, and the
+  // regions of small groups cost up to several times the average.
+  bool static_done = false;
+  for (;;) {
+  uint64_t r, rend;
+  if (a.nwchunks) {
+    uint32_t c = 0;
+    if (lane == 0) c = atomicAdd(a.wctr, 1u);  // (vector atomic, one lane)
+    c = uni(c);
+    if (c >= a.nwchunks) break;
+    r = uni64(a.wchunks[c]);
+    rend = uni64(a.wchunks[c + 1]);
+  } else {
+    if (static_done) break;
+    static_done = true;
+    const uint64_t nwaves = (uint64_t)gridDim.x * WPB;
+    const uint64_t gw = (uint64_t)blockIdx.x * WPB + wid;
+    const uint64_t total = a.re - a.rb;
+    r = uni64(a.rb + (uint64_t)(((unsigned __int128)total * gw) / nwaves));
+    rend = uni64(a.rb + (uint64_t)(((unsigned __int128)total * (gw + 1)) / nwaves));
+  }
 
   if (r < rend) {
     uint32_t hq[F];  // fixed positions p_3 .. p_{N-1} (uniform)
@@ -533,7 +551,7 @@ __global__ void __launch_bounds__(GROUP_MAX_BD, GCfg<N>::PERM ? BOTE_GROUP_WAVES
         if constexpr (PERM) {
           const uint64_t nk = __ballot(have && ((cur & 0xFFu) == 0 || lane == 0));
           const uint32_t nsl = (uint32_t)__popcll(nk);
-          use_lines = nsl <= a.gslots;
+          use_lines = nsl <= a.gslots && !ABLATE(a, 4096);
           if (use_lines) {
             // slot = index of the lane's pair among the step's pairs; the
             // first lane of each pair publishes its key to the wave's slot table
@@ -631,7 +649,16 @@ __global__ void __launch_bounds__(GROUP_MAX_BD, GCfg<N>::PERM ? BOTE_GROUP_WAVES
             //      row = its sorted fixed part + the 2 distances to the other
             //      variable members; each fixed row = the group's sorted
             //      fixed-to-fixed list + the lane's 3 distances (packed)
-            const uint4 X0 = l128(rxt + 16 * pv[0]), X1 = l128(rxt + 16 * pv[1]), X2 = l128(rxt + 16 * pv[2]);
+            uint4 X0, X1, X2;
+            if (ABLATE(a, 8192)) {  // timing only: no table reads
+              X0 = make_uint4(pv[0], pv[1], pv[2], pv[0] ^ pv[1]);
+              X1 = make_uint4(pv[2], pv[0], pv[1], pv[1] ^ pv[2]);
+              X2 = make_uint4(pv[1], pv[2], pv[0], pv[0] ^ pv[2]);
+            } else {
+              X0 = l128(rxt + 16 * pv[0]);
+              X1 = l128(rxt + 16 * pv[1]);
+              X2 = l128(rxt + 16 * pv[2]);
+            }
             {  // rows 0 and 1, packed (lo: member 0, hi: member 1)
               us2 A[4], y[2], L[KQ];
               A[0] = as_us2(__builtin_amdgcn_perm(X1.x, X0.x, 0x05040100u));
@@ -1196,6 +1223,8 @@ __global__ void __launch_bounds__(GROUP_MAX_BD, GCfg<N>::PERM ? BOTE_GROUP_WAVES
       }
       wave_sync();  // the group line is rewritten next
     }
+  }
+  wave_sync();  // (the next chunk rewrites the group line)
   }
   if (valid_cnt) atomicAdd(&a.out_counters[0], (unsigned long long)valid_cnt);
   if (digest) atomicAdd(&a.out_counters[1], (unsigned long long)digest);

@@ -94,6 +94,12 @@ struct FastArgs {
   uint32_t gqsh;      // group kernel: log2 of the qtab plane stride in bytes (1 << gqsh >= gbd * 4)
   uint32_t gslots;    // group kernel, n <= 7: client lines per wave (0: none), see bote_group.hip
   uint32_t grx;       // group kernel, n <= 7: per-group position table (1) or per-lane row sorts (0)
+  // group kernel work distribution: nwchunks > 0: waves take cost-balanced
+  // rank chunks [wchunks[c], wchunks[c+1]) from the ticket counter *wctr
+  // (zeroed before each launch); 0: each wave sweeps an equal share of ranks
+  const uint64_t* wchunks;
+  uint32_t nwchunks;
+  unsigned int* wctr;
   int want_score, p_int;
   int64_t p1i, p2i;  // p_int: min_mean_{fpaxos,epaxos}_improv * nc as integers
   double p_fmean, p_emean;
