@@ -215,7 +215,13 @@ double group_utilisation(uint32_t ns, uint32_t n) {
 // wavefront steps plus GROUP_COST steps of per-group precompute for the part
 // of it inside the range.  Returns nchunks + 1 boundaries, or nothing when the
 // range has too many groups to walk (the kernel then splits ranks evenly).
-constexpr double GROUP_COST = 1.5;
+#ifndef BOTE_GROUP_COST
+#define BOTE_GROUP_COST 1.5
+#endif
+#ifndef BOTE_CHUNKS_PER_WAVE
+#define BOTE_CHUNKS_PER_WAVE 32
+#endif
+constexpr double GROUP_COST = BOTE_GROUP_COST;
 constexpr uint64_t MAX_WALK_GROUPS = 40000000;
 std::vector<uint64_t> group_chunks(uint32_t ns, uint32_t n, uint64_t rb, uint64_t re, uint32_t nchunks) {
   std::vector<uint64_t> out;
@@ -1015,7 +1021,7 @@ static int launch_fast_path(bote_sweep* s, uint64_t rb, uint64_t re, hipStream_t
   HIP_TRY(hipMemsetAsync(s->counters.p, 0, 16, st));
   HIP_TRY(hipMemsetAsync(s->qcount.p, 0, 8, st));
   if (s->group) {
-    // cost-balanced chunks, 4 per wave, taken dynamically (bote_group.hip)
+    // cost-balanced chunks (32 per wave), taken dynamically (bote_group.hip)
     auto key = std::make_pair(rb, re);
     auto it = s->chunks.find(key);
     if (it == s->chunks.end()) {
@@ -1026,7 +1032,9 @@ static int launch_fast_path(bote_sweep* s, uint64_t rb, uint64_t re, hipStream_t
       }
       auto c = std::make_unique<bote_sweep::Chunks>();
       const uint32_t nwaves = s->fgrid * (f.gbd / 64);
-      c->host = group_chunks(s->ns, s->n, rb, re, nwaves * 4);
+      // (no chunk below ~4 wavefront steps of configs)
+      const uint64_t want = std::min<uint64_t>((uint64_t)nwaves * BOTE_CHUNKS_PER_WAVE, (re - rb) / 256 + 1);
+      c->host = group_chunks(s->ns, s->n, rb, re, (uint32_t)want);
       if (!c->host.empty()) {
         c->n = (uint32_t)c->host.size() - 1;
         if (c->dev.alloc(c->host.size() * 8) != hipSuccess) return fail(BOTE_E_NOMEM, "hipMalloc work chunks");
