@@ -564,7 +564,7 @@ __global__ void __launch_bounds__(GROUP_MAX_BD, GCfg<N>::PERM ? BOTE_GROUP_WAVES
             // then lpl lanes per line (one quad = 4 clients each), 64 / lpl
             // lines per pass
             const uint32_t nqq = nq + (rem ? 1u : 0u);
-            const uint32_t lsh = nqq <= 16 ? 4u : (nqq <= 32 ? 5u : 6u), lpl = 1u << lsh;
+            const uint32_t lsh = nqq <= 16 ? 3u : (nqq <= 32 ? 4u : 5u), lpl = 1u << lsh;
             const uint32_t li = lane >> lsh, qx = lane & (lpl - 1);
             for (uint32_t sl = 0; sl < nsl; sl += 64u >> lsh) {
               const uint32_t sx = sl + li;
