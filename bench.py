@@ -166,7 +166,7 @@ def main():
 
     from fantoch_amd import _lib
     from fantoch_amd.bote import DEFAULT_OBJECTIVES, DEFAULT_RANKING, DevicePlanet, Sweep
-    from fantoch_amd.dist import shard_range, sharded_sweep
+    from fantoch_amd.dist import shard_of, sharded_sweep
     from fantoch_amd.planet import Planet
 
     wl = workloads()[args.workload]
@@ -178,7 +178,7 @@ def main():
     # checksum, so none of compute_stats' work can be skipped.
     sweep = Sweep(dp, srv, srv, n, DEFAULT_OBJECTIVES, K=100, ranking=DEFAULT_RANKING, digest=True)
     total = sweep.total
-    b, e = shard_range(total, world, rank)
+    b, e = shard_of(sweep, world, rank)  # equal estimated cost (bote_sweep_split)
     stream = torch.cuda.current_stream().cuda_stream
 
     def step():

@@ -38,7 +38,7 @@ EXPORTS = [
     "bote_sweep_create", "bote_sweep_launch", "bote_sweep_result", "bote_sweep_result_bytes",
     "bote_sweep_result_device", "bote_merge_device", "bote_sweep_last_kernel_ms",
     "bote_sweep_destroy", "bote_colex_unrank", "bote_binomial", "bote_sweep_timing_reset",
-    "bote_sweep_timing", "bote_sweep_grid", "bote_sweep_is_fast", "bote_sweep_create_ex", "bote_search_topk", "bote_sweep_deferred", "bote_eval_leaderless", "bote_evolving_chains",
+    "bote_sweep_timing", "bote_sweep_grid", "bote_sweep_is_fast", "bote_sweep_split", "bote_sweep_create_ex", "bote_search_topk", "bote_sweep_deferred", "bote_eval_leaderless", "bote_evolving_chains",
 ]
 KERNELS = {None: 0, "auto": 0, "generic": 1, "fast": 2, "group": 3}
 
@@ -136,6 +136,7 @@ def lib():
     L.bote_sweep_timing.argtypes = [_vp, C.POINTER(C.c_float), C.POINTER(C.c_uint32)]
     L.bote_sweep_grid.argtypes = [_vp, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
     L.bote_sweep_is_fast.argtypes = [_vp, C.POINTER(C.c_int)]
+    L.bote_sweep_split.argtypes = [_vp, C.c_uint64, C.c_uint64, C.c_uint32, C.POINTER(C.c_uint64)]
     L.bote_sweep_deferred.argtypes = [_vp, _vp, C.POINTER(C.c_uint64)]
     L.bote_colex_unrank.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32, _u32p]
     L.bote_binomial.restype = C.c_uint64

@@ -807,6 +807,17 @@ class Sweep:
         check(lib().bote_sweep_is_fast(self.h, C.byref(v)))
         return ("generic", "fast", "group")[v.value]
 
+    def split(self, rank_begin: int, rank_end: int, parts: int) -> List[int]:
+        """Shard boundaries of equal estimated cost (bote_sweep_split):
+        parts + 1 ascending ranks from rank_begin to rank_end."""
+        cache = self.__dict__.setdefault("_splits", {})
+        key = (rank_begin, rank_end, parts)
+        if key not in cache:  # (a host walk of the groups: ms at R=64 n=7)
+            out = (C.c_uint64 * (parts + 1))()
+            check(lib().bote_sweep_split(self.h, rank_begin, rank_end, parts, out))
+            cache[key] = [int(x) for x in out]
+        return list(cache[key])
+
     def geometry(self) -> Tuple[int, int, int]:
         g, b, l = C.c_uint32(), C.c_uint32(), C.c_uint32()
         check(lib().bote_sweep_grid(self.h, C.byref(g), C.byref(b), C.byref(l)))

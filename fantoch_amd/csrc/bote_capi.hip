@@ -939,6 +939,23 @@ int bote_sweep_is_fast(const bote_sweep* s, int* out) {
   return BOTE_OK;
 }
 
+int bote_sweep_split(const bote_sweep* s, uint64_t rank_begin, uint64_t rank_end, uint32_t parts,
+                     uint64_t* out_bounds) {
+  if (!s || !out_bounds) return fail(BOTE_E_ARG, "null argument");
+  if (parts == 0) return fail(BOTE_E_ARG, "parts must be >= 1");
+  if (rank_begin > rank_end || rank_end > binom_u64(s->ns, s->n)) return fail(BOTE_E_ARG, "rank range out of bounds");
+  std::vector<uint64_t> b;
+  if (s->fast && s->group && rank_end - rank_begin >= (uint64_t)parts * 64)
+    b = group_chunks(s->ns, s->n, rank_begin, rank_end, parts);
+  if (b.size() != (size_t)parts + 1) {
+    b.resize((size_t)parts + 1);
+    const uint64_t span = rank_end - rank_begin;
+    for (uint32_t i = 0; i <= parts; ++i) b[i] = rank_begin + (uint64_t)(((unsigned __int128)span * i) / parts);
+  }
+  std::copy(b.begin(), b.end(), out_bounds);
+  return BOTE_OK;
+}
+
 // Merge `lists` per-block lists into the result block and append the counters.
 // With `sel` (fast path), the first level reads the overflow fallback's
 // `alt_lists` lists and counters instead when *sel > QUEUE_CAP (on the device).
@@ -1282,12 +1299,11 @@ int bote_search_topk(const bote_planet* const* planets, uint32_t n_devices, cons
         hipEventCreateWithFlags(&sh[i].done, hipEventDisableTiming) != hipSuccess)
       return cleanup(fail(BOTE_E_DEVICE, "shard stream/event"));
   }
-  const uint64_t span = rank_end - rank_begin;
-  for (uint32_t i = 0; i < n_devices; ++i) {
-    const uint64_t b = rank_begin + (uint64_t)(((unsigned __int128)span * i) / n_devices);
-    const uint64_t e = rank_begin + (uint64_t)(((unsigned __int128)span * (i + 1)) / n_devices);
-    if ((rc = bote_sweep_launch(sh[i].sw, b, e, sh[i].st))) return cleanup(rc);
-  }
+  // shards of equal estimated cost (bote_sweep_split)
+  std::vector<uint64_t> bnd((size_t)n_devices + 1);
+  if ((rc = bote_sweep_split(sh[0].sw, rank_begin, rank_end, n_devices, bnd.data()))) return cleanup(rc);
+  for (uint32_t i = 0; i < n_devices; ++i)
+    if ((rc = bote_sweep_launch(sh[i].sw, bnd[i], bnd[i + 1], sh[i].st))) return cleanup(rc);
   // gather on the root device
   const uint64_t nb = sh[0].sw->result_bytes();
   if (hipSetDevice(root) != hipSuccess || hipStreamCreateWithFlags(&rst, hipStreamNonBlocking) != hipSuccess ||

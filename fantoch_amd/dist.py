@@ -14,10 +14,26 @@ from typing import Tuple
 
 
 def shard_range(total: int, world: int, rank: int) -> Tuple[int, int]:
-    """Contiguous, balanced split of [0, total) (per-config cost is constant)."""
+    """Contiguous split of [0, total) into equal rank counts."""
     if world < 1 or not 0 <= rank < world:
         raise ValueError(f"bad shard {rank} of {world}")
     return total * rank // world, total * (rank + 1) // world
+
+
+def shard_of(sweep, world: int, rank: int) -> Tuple[int, int]:
+    """This rank's contiguous shard of [0, sweep.total).  Rank shares of equal
+    size are not equal work on the group kernel (small groups cost more per
+    config), so a sweep that offers `split` (bote_sweep_split) is cut into
+    shards of equal estimated cost; anything else into equal rank counts."""
+    if world < 1 or not 0 <= rank < world:
+        raise ValueError(f"bad shard {rank} of {world}")
+    split = getattr(sweep, "split", None)
+    if world == 1:
+        return 0, sweep.total
+    if split is None:
+        return shard_range(sweep.total, world, rank)
+    b = split(0, sweep.total, world)
+    return b[rank], b[rank + 1]
 
 
 def _device_of(sweep, device):
@@ -43,7 +59,7 @@ def sharded_sweep(sweep, stream=None, group=None, device=None):
 
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     rank = dist.get_rank(group) if dist.is_initialized() else 0
-    b, e = shard_range(sweep.total, world, rank)
+    b, e = shard_of(sweep, world, rank)
     device = _device_of(sweep, device)
     if stream is None and device.type == "cuda":
         stream = torch.cuda.current_stream(device).cuda_stream

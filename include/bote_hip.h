@@ -255,6 +255,16 @@ int bote_sweep_timing(bote_sweep* s, float* out_total_ms, uint32_t* out_launches
  * packed fast-path kernel (bote_sweep.hip), 2 the group kernel
  * (bote_group.hip).  All are exact (DESIGN.md "Kernels"). */
 int bote_sweep_is_fast(const bote_sweep* s, int* out);
+/* Shard boundaries for `parts` devices over [rank_begin, rank_end): out[0] =
+ * rank_begin, out[parts] = rank_end, ascending.  On the group kernel the
+ * shards have equal estimated cost (a group of C(p, 3) configs costs
+ * ceil(C(p, 3) / 64) wavefront steps plus its precompute; equal rank shares
+ * of R=64 n=7 differ by up to 14 % over 8 devices), otherwise equal rank
+ * counts.  Host only (no device work).  Replaces the reference's split of
+ * work, a rayon fork-join over client sets (fantoch_bote/src/search.rs:209-231):
+ * here one client set's rank space is split. */
+int bote_sweep_split(const bote_sweep* s, uint64_t rank_begin, uint64_t rank_end, uint32_t parts,
+                     uint64_t* out_bounds);
 /* Configs the fast/group kernel deferred to the exact generic kernel in the
  * last launch (COV near-ties; more than 2^20 => the whole range was recomputed
  * on the generic path).  Synchronises `hip_stream`.  0 on the generic path. */

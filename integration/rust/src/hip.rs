@@ -94,6 +94,8 @@ extern "C" {
                                 out: *mut *mut bote_sweep) -> c_int;
     pub fn bote_sweep_launch(s: *mut bote_sweep, rank_begin: u64, rank_end: u64, stream: *mut c_void) -> c_int;
     pub fn bote_sweep_deferred(s: *mut bote_sweep, stream: *mut c_void, out: *mut u64) -> c_int;
+    pub fn bote_sweep_split(s: *const bote_sweep, rank_begin: u64, rank_end: u64, parts: u32,
+                            out_bounds: *mut u64) -> c_int;
     pub fn bote_eval_leaderless(p: *const bote_planet, servers: *const u32, ns: u32, clients: *const u32, nc: u32,
                                 n: u32, configs: *const u32, rank_begin: u64, ncfg: u64, quorum_sizes: *const u32,
                                 nq: u32, out_vals: *mut u32, out_sum: *mut u64, out_sumsq: *mut u64) -> c_int;

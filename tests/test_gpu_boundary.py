@@ -170,3 +170,38 @@ def test_tempo_stats_keys_and_unsorted_configs():
             assert list(st.get(proto, f, ClientPlacement.Input).iter_values()) == want_i
             assert list(st.get(proto, f, ClientPlacement.Colocated).iter_values()) == want_c
         assert "af1" in st.map and "e" in st.map  # the reference's keys are still there
+
+
+def test_sweep_split_bounds():
+    """bote_sweep_split: ascending bounds covering the range; on the group
+    kernel the first shard of R=64 n=7 (the small-group region, more work per
+    config) gets fewer ranks than an equal share; shards swept separately and
+    merged equal the oracle's full-sweep fixture."""
+    import torch
+
+    from fantoch_amd.dist import merge_gathered
+
+    p = Planet.synthetic(64)
+    dp = DevicePlanet(p)
+    srv = np.arange(64, dtype=np.uint32)
+    sw = Sweep(dp, srv, srv, 7, DEFAULT_OBJECTIVES, K=100, ranking=DEFAULT_RANKING, digest=True)
+    assert sw.kernel_path() == "group"
+    b = sw.split(0, sw.total, 8)
+    assert b[0] == 0 and b[-1] == sw.total and all(x < y for x, y in zip(b, b[1:]))
+    assert b[1] < sw.total // 8
+    assert sw.split(100, 100, 3) == [100] * 4
+    g = sw.split(5, 1000, 4)
+    assert g[0] == 5 and g[-1] == 1000 and g == sorted(g)
+    path = os.path.join(GOLDEN, "syn_r64n7_full.json")
+    if not os.path.exists(path):
+        pytest.skip("full fixture not generated")
+    fx = json.load(open(path))
+    nb = sw.result_bytes()
+    gathered = torch.empty(8 * nb, dtype=torch.uint8, device="cuda")
+    stream = torch.cuda.current_stream().cuda_stream
+    for i in range(8):
+        sw.launch(b[i], b[i + 1], stream)
+        sw.result_device(gathered.data_ptr() + i * nb, stream)
+    got = merge_gathered(sw, gathered, 8)
+    assert (got.valid, got.digest) == (fx["valid"], fx["digest"])
+    assert got.tops == [[tuple(r) for r in t] for t in fx["tops"]]
