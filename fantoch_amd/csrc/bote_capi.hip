@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -216,16 +217,25 @@ double group_utilisation(uint32_t ns, uint32_t n) {
 // of it inside the range.  Returns nchunks + 1 boundaries, or nothing when the
 // range has too many groups to walk (the kernel then splits ranks evenly).
 #ifndef BOTE_GROUP_COST
-#define BOTE_GROUP_COST 1.5
+#define BOTE_GROUP_COST 0.0  // 0: fitted per client count (group_cost)
 #endif
 #ifndef BOTE_CHUNKS_PER_WAVE
 #define BOTE_CHUNKS_PER_WAVE 32
 #endif
-constexpr double GROUP_COST = BOTE_GROUP_COST;
+// One group's precompute in wavefront steps, least-squares fitted to the
+// per-shard kernel times of scripts/shard_balance.py (profiles/r02h_*): 0.64
+// at 64 clients (n=7), 3.7 at 128 clients (n=6); interpolated as a power of
+// the client count in between and clamped outside.
+double group_cost(uint32_t nc) {
+  if (BOTE_GROUP_COST > 0) return BOTE_GROUP_COST;
+  const double c = 0.64 * std::pow((double)nc / 64.0, 2.53);
+  return std::min(8.0, std::max(0.25, c));
+}
 constexpr uint64_t MAX_WALK_GROUPS = 40000000;
-std::vector<uint64_t> group_chunks(uint32_t ns, uint32_t n, uint64_t rb, uint64_t re, uint32_t nchunks) {
+std::vector<uint64_t> group_chunks(uint32_t ns, uint32_t n, uint32_t nc, uint64_t rb, uint64_t re, uint32_t nchunks) {
   std::vector<uint64_t> out;
   if (re <= rb || n < 4 || nchunks == 0) return out;
+  const double GROUP_COST = group_cost(nc);
   const uint32_t F = n - 3;
   // colex unrank of rb: p[j] = the largest m with C(m, j + 1) <= rest
   std::vector<uint32_t> p(n);
@@ -946,7 +956,7 @@ int bote_sweep_split(const bote_sweep* s, uint64_t rank_begin, uint64_t rank_end
   if (rank_begin > rank_end || rank_end > binom_u64(s->ns, s->n)) return fail(BOTE_E_ARG, "rank range out of bounds");
   std::vector<uint64_t> b;
   if (s->fast && s->group && rank_end - rank_begin >= (uint64_t)parts * 64)
-    b = group_chunks(s->ns, s->n, rank_begin, rank_end, parts);
+    b = group_chunks(s->ns, s->n, s->nc, rank_begin, rank_end, parts);
   if (b.size() != (size_t)parts + 1) {
     b.resize((size_t)parts + 1);
     const uint64_t span = rank_end - rank_begin;
@@ -1051,7 +1061,7 @@ static int launch_fast_path(bote_sweep* s, uint64_t rb, uint64_t re, hipStream_t
       const uint32_t nwaves = s->fgrid * (f.gbd / 64);
       // (no chunk below ~4 wavefront steps of configs)
       const uint64_t want = std::min<uint64_t>((uint64_t)nwaves * BOTE_CHUNKS_PER_WAVE, (re - rb) / 256 + 1);
-      c->host = group_chunks(s->ns, s->n, rb, re, (uint32_t)want);
+      c->host = group_chunks(s->ns, s->n, s->nc, rb, re, (uint32_t)want);
       if (!c->host.empty()) {
         c->n = (uint32_t)c->host.size() - 1;
         if (c->dev.alloc(c->host.size() * 8) != hipSuccess) return fail(BOTE_E_NOMEM, "hipMalloc work chunks");
