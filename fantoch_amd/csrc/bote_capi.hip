@@ -853,6 +853,15 @@ int bote_sweep_create_ex(const bote_planet* p, const uint32_t* servers, uint32_t
     f.p_int = integral(a.p_fmean) && integral(a.p_emean) ? 1 : 0;
     f.p1i = f.p_int ? (int64_t)a.p_fmean * (int64_t)nc : 0;
     f.p2i = f.p_int ? (int64_t)a.p_emean * (int64_t)nc : 0;
+    auto band = [&](double p, int64_t pi, int32_t& lo, int32_t& hi) {
+      const double t = p * (double)nc;
+      const double l = f.p_int ? (double)pi : std::floor(t) - 1.0, h = f.p_int ? (double)pi : std::ceil(t) + 1.0;
+      const double cap = 2147483647.0;  // D = a difference of two sums below 2^21
+      lo = (int32_t)std::max(-cap, std::min(cap, l));
+      hi = (int32_t)std::max(-cap, std::min(cap, h));
+    };
+    band(a.p_fmean, f.p1i, f.m1_lo, f.m1_hi);
+    band(a.p_emean, f.p2i, f.m2_lo, f.m2_hi);
     f.n_obj = a.n_obj;
     for (int o = 0; o < bote::MAXOBJ; ++o) {
       f.obj_kind[o] = a.obj_kind[o];

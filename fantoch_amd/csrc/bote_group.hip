@@ -1077,24 +1077,23 @@ __global__ void __launch_bounds__(GROUP_MAX_BD, GCfg<N>::PERM ? BOTE_GROUP_WAVES
               bool valid = false;
               const int fcap = min(N / 2, a.ft_metric);
               bool defer = false;
-              if (a.want_score && !ABLATE(a, 256)) {
+              if (!ABLATE(a, 256)) {  // (the default objectives imply want_score)
                 valid = true;
 #pragma unroll
                 for (int f = 1; f <= 2; ++f) {
                   if (f > fcap) break;
                   const Mom& ma = mom[f == 1 ? SLOT_AF1 : SLOT_AF2];
                   const Mom& mf = mom[f == 1 ? SLOT_FF1 : SLOT_FF2];
-                  // fmi >= p1: integers unless the sums meet exactly
+                  // fmi >= p1: decided on the integer difference outside
+                  // [m1_lo, m1_hi], by the reference's f64 arithmetic inside
                   const int32_t D = (int32_t)((uint32_t)mf.s1 - (uint32_t)ma.s1);
-                  bool mok;
-                  if (a.p_int && (int64_t)D != a.p1i) mok = (int64_t)D > a.p1i;
-                  else mok = (mom_mean(mf) - mom_mean(ma)) >= a.p_fmean;
+                  bool mok = D > a.m1_hi;
+                  if (D >= a.m1_lo && D <= a.m1_hi) mok = (mom_mean(mf) - mom_mean(ma)) >= a.p_fmean;
                   valid = valid && mok;
                   if (N == 11 || N == 13) {
                     const int32_t De = (int32_t)((uint32_t)mom[SLOT_E].s1 - (uint32_t)ma.s1);
-                    bool eok;
-                    if (a.p_int && (int64_t)De != a.p2i) eok = (int64_t)De > a.p2i;
-                    else eok = (mom_mean(mom[SLOT_E]) - mom_mean(ma)) >= a.p_emean;
+                    bool eok = De > a.m2_hi;
+                    if (De >= a.m2_lo && De <= a.m2_hi) eok = (mom_mean(mom[SLOT_E]) - mom_mean(ma)) >= a.p_emean;
                     valid = valid && eok;
                   }
                 }

@@ -102,6 +102,10 @@ struct FastArgs {
   unsigned int* wctr;
   int want_score, p_int;
   int64_t p1i, p2i;  // p_int: min_mean_{fpaxos,epaxos}_improv * nc as integers
+  // group kernel mean tests on D = the integer difference of two sums: true
+  // above hi, false below lo, the reference's f64 arithmetic in [lo, hi]
+  // (lo = hi = p1i when p_int; otherwise floor/ceil of p * nc -/+ 1)
+  int32_t m1_lo, m1_hi, m2_lo, m2_hi;
   double p_fmean, p_emean;
   int ft_metric;
   int n_obj;
