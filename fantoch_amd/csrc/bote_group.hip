@@ -326,9 +326,13 @@ __device__ __forceinline__ float u64_to_f32(uint64_t x) {
 // DEF: the default objective set (bote.py DEFAULT_OBJECTIVES: SCORE, MEAN af1,
 // MEAN ff1, COV af1, MEAN e), compiled in; otherwise the objectives come from
 // the arguments (finish_config, bote_fast.hpp).
-template <int N, bool DEF>
+// SI: the servers are the planet's regions in order (srv[p] == p), compiled
+// in for the default objectives (the bench sweeps): the position -> region
+// lookups vanish, and with them uniform masks the kernel had spilled
+template <int N, bool DEF, bool SI>
 __global__ void __launch_bounds__(GROUP_MAX_BD, GCfg<N>::PERM ? BOTE_GROUP_WAVES_PERM : BOTE_GROUP_WAVES)
     sweep_group_kernel(FastArgs a) {
+  const bool sid = SI || a.srv_identity;
   using QC = QCfg<N>;
   using GC = GCfg<N>;
   constexpr int NL = QC::NL;
@@ -458,7 +462,7 @@ __global__ void __launch_bounds__(GROUP_MAX_BD, GCfg<N>::PERM ? BOTE_GROUP_WAVES
       // ---------------- per-group, wave-uniform precompute -> group line
       uint32_t freg[F];
 #pragma unroll
-      for (int k = 0; k < F; ++k) freg[k] = uni(a.srv_identity ? hq[k] : srv[hq[k]]);
+      for (int k = 0; k < F; ++k) freg[k] = uni(sid ? hq[k] : srv[hq[k]]);
       if (lane < (uint32_t)F) {
         uint32_t pos = 0;
 #pragma unroll
@@ -507,7 +511,7 @@ __global__ void __launch_bounds__(GROUP_MAX_BD, GCfg<N>::PERM ? BOTE_GROUP_WAVES
         // fixed members (row part), the fixed members' distances to x
         // (column part, packed as the fixed-row pairs); absent members INF
         for (uint32_t x = lane; x < hq[0]; x += 64) {
-          const uint32_t rg = a.srv_identity ? x : srv[x];
+          const uint32_t rg = sid ? x : srv[x];
           uint32_t rf[4], cf[4];
 #pragma unroll
           for (int k = 0; k < 4; ++k) {
@@ -571,8 +575,8 @@ __global__ void __launch_bounds__(GROUP_MAX_BD, GCfg<N>::PERM ? BOTE_GROUP_WAVES
               if (sx < nsl) {
                 const uint32_t k = l32(keys + 4 * sx);
                 const uint32_t p1 = (k >> 8) & 0xFFu, p2 = k >> 16;
-                const uint32_t b1 = cqt + (a.srv_identity ? p1 : srv[p1]) * cstride;
-                const uint32_t b2 = cqt + (a.srv_identity ? p2 : srv[p2]) * cstride;
+                const uint32_t b1 = cqt + (sid ? p1 : srv[p1]) * cstride;
+                const uint32_t b2 = cqt + (sid ? p2 : srv[p2]) * cstride;
                 const uint32_t dst = lines + sx * cstride;
                 for (uint32_t x = qx; x < nqq; x += lpl) {
                   const uint2 v1 = l64(b1 + 8 * x), v2 = l64(b2 + 8 * x), vf = l64(mfl + 8 * x);
@@ -591,7 +595,7 @@ __global__ void __launch_bounds__(GROUP_MAX_BD, GCfg<N>::PERM ? BOTE_GROUP_WAVES
           pv[1] = (cur >> 8) & 0xFF;
           pv[2] = cur >> 16;
 #pragma unroll
-          for (int i = 0; i < 3; ++i) rv[i] = a.srv_identity ? pv[i] : srv[pv[i]];
+          for (int i = 0; i < 3; ++i) rv[i] = sid ? pv[i] : srv[pv[i]];
           uint32_t cv[3];  // RQT column of each variable member
 #pragma unroll
           for (int i = 0; i < 3; ++i) cv[i] = rqt + rv[i] * rstride;
@@ -1236,9 +1240,9 @@ __global__ void __launch_bounds__(GROUP_MAX_BD, GCfg<N>::PERM ? BOTE_GROUP_WAVES
 }
 
 // ------------------------------------------------------------- launcher ---
-template <int N, bool DEF>
+template <int N, bool DEF, bool SI>
 static hipError_t launch_group_n(const FastArgs& a, uint32_t grid, size_t shm, hipStream_t st) {
-  auto k = sweep_group_kernel<N, DEF>;
+  auto k = sweep_group_kernel<N, DEF, SI>;
   hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k, dim3(grid), dim3(a.gbd), shm, st, a);
@@ -1248,7 +1252,7 @@ static hipError_t launch_group_n(const FastArgs& a, uint32_t grid, size_t shm, h
 static const void* group_fn(uint32_t n, bool def) {
   switch (n) {
 #define FN_CASE(NN) \
-  case NN: return def ? (const void*)sweep_group_kernel<NN, true> : (const void*)sweep_group_kernel<NN, false>;
+  case NN: return def ? (const void*)sweep_group_kernel<NN, true, false> : (const void*)sweep_group_kernel<NN, false, false>;
     FN_CASE(4) FN_CASE(5) FN_CASE(6) FN_CASE(7) FN_CASE(8) FN_CASE(9) FN_CASE(10) FN_CASE(11) FN_CASE(12)
     FN_CASE(13) FN_CASE(14) FN_CASE(15) FN_CASE(16)
 #undef FN_CASE
@@ -1268,7 +1272,10 @@ int group_occupancy(uint32_t n, size_t shm, bool def, uint32_t bd) {
 hipError_t launch_group(const FastArgs& a, uint32_t n, bool def, uint32_t grid, size_t shm, hipStream_t st) {
   switch (n) {
 #define GS_CASE(NN) \
-  case NN: return def ? launch_group_n<NN, true>(a, grid, shm, st) : launch_group_n<NN, false>(a, grid, shm, st);
+  case NN:                                                                                           \
+    return def ? (a.srv_identity ? launch_group_n<NN, true, true>(a, grid, shm, st)                  \
+                                 : launch_group_n<NN, true, false>(a, grid, shm, st))                \
+               : launch_group_n<NN, false, false>(a, grid, shm, st);
     GS_CASE(4) GS_CASE(5) GS_CASE(6) GS_CASE(7) GS_CASE(8) GS_CASE(9) GS_CASE(10) GS_CASE(11) GS_CASE(12)
     GS_CASE(13) GS_CASE(14) GS_CASE(15) GS_CASE(16)
 #undef GS_CASE
