@@ -326,9 +326,10 @@ __device__ __forceinline__ float u64_to_f32(uint64_t x) {
 // DEF: the default objective set (bote.py DEFAULT_OBJECTIVES: SCORE, MEAN af1,
 // MEAN ff1, COV af1, MEAN e), compiled in; otherwise the objectives come from
 // the arguments (finish_config, bote_fast.hpp).
-// SI: the servers are the planet's regions in order (srv[p] == p), compiled
-// in for the default objectives (the bench sweeps): the position -> region
-// lookups vanish, and with them uniform masks the kernel had spilled
+// SI ("bench-shaped" default-objective sweeps): the servers are the planet's
+// regions in order (srv[p] == p), the digest is on and ft_metric is F1F2,
+// compiled in: the position -> region lookups and the flag tests vanish, and
+// with them uniform masks the kernel had spilled to VGPR lanes
 template <int N, bool DEF, bool SI>
 __global__ void __launch_bounds__(GROUP_MAX_BD, GCfg<N>::PERM ? BOTE_GROUP_WAVES_PERM : BOTE_GROUP_WAVES)
     sweep_group_kernel(FastArgs a) {
@@ -1079,7 +1080,7 @@ __global__ void __launch_bounds__(GROUP_MAX_BD, GCfg<N>::PERM ? BOTE_GROUP_WAVES
               //      for configs that pass them, and a config is deferred
               //      only when its validity hinges on an ambiguous COV call.
               bool valid = false;
-              const int fcap = min(N / 2, a.ft_metric);
+              const int fcap = min(N / 2, SI ? 2 : a.ft_metric);
               bool defer = false;
               if (!ABLATE(a, 256)) {  // (the default objectives imply want_score)
                 valid = true;
@@ -1126,7 +1127,7 @@ __global__ void __launch_bounds__(GROUP_MAX_BD, GCfg<N>::PERM ? BOTE_GROUP_WAVES
                 defer_rank(a, rank);
               } else {
                 if (valid) ++valid_cnt;
-                if (a.want_digest && !ABLATE(a, 16)) {
+                if ((SI || a.want_digest) && !ABLATE(a, 16)) {
                   uint32_t h = 0;
 #pragma unroll
                   for (int sl = 0; sl < NSLOT; ++sl) h = digest_fold(h, mom[sl].s1, mom[sl].s2);
@@ -1273,7 +1274,8 @@ hipError_t launch_group(const FastArgs& a, uint32_t n, bool def, uint32_t grid, 
   switch (n) {
 #define GS_CASE(NN) \
   case NN:                                                                                           \
-    return def ? (a.srv_identity ? launch_group_n<NN, true, true>(a, grid, shm, st)                  \
+    return def ? (a.srv_identity && a.want_digest && a.ft_metric == 2                               \
+                      ? launch_group_n<NN, true, true>(a, grid, shm, st)                              \
                                  : launch_group_n<NN, true, false>(a, grid, shm, st))                \
                : launch_group_n<NN, false, false>(a, grid, shm, st);
     GS_CASE(4) GS_CASE(5) GS_CASE(6) GS_CASE(7) GS_CASE(8) GS_CASE(9) GS_CASE(10) GS_CASE(11) GS_CASE(12)
