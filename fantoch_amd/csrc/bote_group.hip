@@ -330,10 +330,12 @@ __device__ __forceinline__ float u64_to_f32(uint64_t x) {
 // regions in order (srv[p] == p), the digest is on and ft_metric is F1F2,
 // compiled in: the position -> region lookups and the flag tests vanish, and
 // with them uniform masks the kernel had spilled to VGPR lanes
-template <int N, bool DEF, bool SI>
+template <int N, bool DEF, bool SI, bool RXC>
 __global__ void __launch_bounds__(GROUP_MAX_BD, GCfg<N>::PERM ? BOTE_GROUP_WAVES_PERM : BOTE_GROUP_WAVES)
     sweep_group_kernel(FastArgs a) {
   const bool sid = SI || a.srv_identity;
+  // the position table: a launch argument, compiled in (RXC) on SI kernels
+  const bool use_rx = GCfg<N>::RX && (SI ? RXC : a.grx != 0);
   using QC = QCfg<N>;
   using GC = GCfg<N>;
   constexpr int NL = QC::NL;
@@ -507,7 +509,7 @@ __global__ void __launch_bounds__(GROUP_MAX_BD, GCfg<N>::PERM ? BOTE_GROUP_WAVES
         }
         s16(mfl + 2 * c, key);
       }
-      if (GC::RX && a.grx) {
+      if (use_rx) {
         // positions below the smallest fixed one: sorted distances to the
         // fixed members (row part), the fixed members' distances to x
         // (column part, packed as the fixed-row pairs); absent members INF
@@ -649,7 +651,7 @@ __global__ void __launch_bounds__(GROUP_MAX_BD, GCfg<N>::PERM ? BOTE_GROUP_WAVES
               }
             }
           };
-          if (GC::RX && a.grx) {
+          if (use_rx) {
             // ---- Q phase from the group's position table: each variable
             //      row = its sorted fixed part + the 2 distances to the other
             //      variable members; each fixed row = the group's sorted
@@ -1241,9 +1243,9 @@ __global__ void __launch_bounds__(GROUP_MAX_BD, GCfg<N>::PERM ? BOTE_GROUP_WAVES
 }
 
 // ------------------------------------------------------------- launcher ---
-template <int N, bool DEF, bool SI>
+template <int N, bool DEF, bool SI, bool RXC>
 static hipError_t launch_group_n(const FastArgs& a, uint32_t grid, size_t shm, hipStream_t st) {
-  auto k = sweep_group_kernel<N, DEF, SI>;
+  auto k = sweep_group_kernel<N, DEF, SI, RXC>;
   hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k, dim3(grid), dim3(a.gbd), shm, st, a);
@@ -1253,7 +1255,7 @@ static hipError_t launch_group_n(const FastArgs& a, uint32_t grid, size_t shm, h
 static const void* group_fn(uint32_t n, bool def) {
   switch (n) {
 #define FN_CASE(NN) \
-  case NN: return def ? (const void*)sweep_group_kernel<NN, true, false> : (const void*)sweep_group_kernel<NN, false, false>;
+  case NN: return def ? (const void*)sweep_group_kernel<NN, true, false, false> : (const void*)sweep_group_kernel<NN, false, false, false>;
     FN_CASE(4) FN_CASE(5) FN_CASE(6) FN_CASE(7) FN_CASE(8) FN_CASE(9) FN_CASE(10) FN_CASE(11) FN_CASE(12)
     FN_CASE(13) FN_CASE(14) FN_CASE(15) FN_CASE(16)
 #undef FN_CASE
@@ -1275,9 +1277,10 @@ hipError_t launch_group(const FastArgs& a, uint32_t n, bool def, uint32_t grid, 
 #define GS_CASE(NN) \
   case NN:                                                                                           \
     return def ? (a.srv_identity && a.want_digest && a.ft_metric == 2                               \
-                      ? launch_group_n<NN, true, true>(a, grid, shm, st)                              \
-                                 : launch_group_n<NN, true, false>(a, grid, shm, st))                \
-               : launch_group_n<NN, false, false>(a, grid, shm, st);
+                      ? (a.grx ? launch_group_n<NN, true, true, true>(a, grid, shm, st)              \
+                               : launch_group_n<NN, true, true, false>(a, grid, shm, st))             \
+                      : launch_group_n<NN, true, false, false>(a, grid, shm, st))                    \
+               : launch_group_n<NN, false, false, false>(a, grid, shm, st);
     GS_CASE(4) GS_CASE(5) GS_CASE(6) GS_CASE(7) GS_CASE(8) GS_CASE(9) GS_CASE(10) GS_CASE(11) GS_CASE(12)
     GS_CASE(13) GS_CASE(14) GS_CASE(15) GS_CASE(16)
 #undef GS_CASE
