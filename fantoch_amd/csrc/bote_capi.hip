@@ -237,6 +237,10 @@ std::vector<uint64_t> group_chunks(uint32_t ns, uint32_t n, uint32_t nc, uint64_
   if (re <= rb || n < 4 || nchunks == 0) return out;
   const double GROUP_COST = group_cost(nc);
   const uint32_t F = n - 3;
+  // too many groups to walk (each group holds at least one config): leave
+  // the range to the even split rather than stall the host
+  const uint64_t all_groups = binom_u64(ns - 3, F);
+  if ((all_groups == 0 || all_groups > MAX_WALK_GROUPS) && re - rb > MAX_WALK_GROUPS) return out;
   // colex unrank of rb: p[j] = the largest m with C(m, j + 1) <= rest
   std::vector<uint32_t> p(n);
   uint64_t rest = rb;
