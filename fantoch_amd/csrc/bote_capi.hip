@@ -902,7 +902,10 @@ int bote_sweep_create_ex(const bote_planet* p, const uint32_t* servers, uint32_t
       // share the client-quad matrix, so R = 128 fits more waves per CU) were
       // measured slower: R=128 n=6 at 640 threads, 5 waves/SIMD, 369 ms vs
       // 348 ms at 256 threads, 2 waves/SIMD.
-      f.gbd = bote::FAST_BD;
+#ifndef BOTE_GROUP_BD
+#define BOTE_GROUP_BD 256
+#endif
+      f.gbd = BOTE_GROUP_BD;
       f.gqsh = 10;
       f.gslots = 0;
       f.grx = 0;
