@@ -92,3 +92,28 @@ def test_shard_range_partition():
             assert max(e - b for b, e in rs) - min(e - b for b, e in rs) <= 1
     with pytest.raises(ValueError):
         shard_range(10, 2, 2)
+
+
+def test_shard_of_uses_the_sweeps_split():
+    """dist.shard_of: one shard is the whole range; a sweep offering `split`
+    (bote_sweep_split: equal estimated cost) is cut there, anything else into
+    equal rank counts."""
+    from fantoch_amd.dist import shard_of
+
+    class Plain:
+        total = 100
+
+    class Split(Plain):
+        calls = 0
+
+        def split(self, rb, re, parts):
+            Split.calls += 1
+            return [rb] + [rb + (re - rb) * (i * i) // (parts * parts) for i in range(1, parts)] + [re]
+
+    assert shard_of(Plain(), 1, 0) == (0, 100)
+    assert [shard_of(Plain(), 4, r) for r in range(4)] == [(0, 25), (25, 50), (50, 75), (75, 100)]
+    assert shard_of(Split(), 1, 0) == (0, 100) and Split.calls == 0
+    got = [shard_of(Split(), 4, r) for r in range(4)]
+    assert got == [(0, 6), (6, 25), (25, 56), (56, 100)]
+    with pytest.raises(ValueError):
+        shard_of(Split(), 2, 2)
