@@ -10,6 +10,14 @@ scaling).  Inputs (the planet, the lists) are resident in HBM before timing.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--workload r64n7|r128n6|gcp]
   N>1: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
+       or python bench.py --gpus N, which starts the N ranks itself
+       (fantoch_amd/launch.py; the launching process never touches the GPU).
+The world size must equal --gpus (the run is refused otherwise), and n_gpus in
+the line is the world that formed, with a census all-gathered over the
+data-path backend as evidence (`world`).
+BOTE_BENCH_REHEARSAL=1 (diagnostics only, never a bench line to quote): N
+ranks share the visible GPUs round-robin and gather over gloo, to rehearse
+the N-rank path on a 1-GPU box; the line is marked "rehearsal".
 """
 import argparse
 import json
@@ -153,6 +161,22 @@ def main():
         if os.environ.get(var):
             sys.exit(f"bench.py: refusing to run with {var} set (diagnostics only)")
 
+    rehearsal = os.environ.get("BOTE_BENCH_REHEARSAL") == "1"
+    if args.gpus < 1:
+        sys.exit("bench.py: --gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # launcher: start the N ranks and exit with their status.  Counting
+        # devices does not initialise HIP (no GPU call in this process).
+        import torch
+
+        ndev = torch.cuda.device_count()
+        if ndev < args.gpus and not (rehearsal and ndev >= 1):
+            sys.exit(f"bench.py: --gpus {args.gpus} but {ndev} GPU(s) visible; refusing to report "
+                     f"{args.gpus} GPUs")
+        from fantoch_amd.launch import run_world
+
+        sys.exit(run_world(args.gpus, [os.path.abspath(__file__)] + sys.argv[1:]))
+
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -160,19 +184,28 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
+    if world != args.gpus:
+        sys.exit(f"bench.py: world size {world} (WORLD_SIZE) != --gpus {args.gpus}; refusing a mislabeled line")
+    ndev = torch.cuda.device_count()
+    if not rehearsal and local >= ndev:
+        sys.exit(f"bench.py rank {rank}: LOCAL_RANK {local} but {ndev} GPU(s) visible")
+    dev_index = local % max(ndev, 1) if rehearsal else local
+    torch.cuda.set_device(dev_index)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if rehearsal:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev_index))
 
     from fantoch_amd import _lib
     from fantoch_amd.bote import DEFAULT_OBJECTIVES, DEFAULT_RANKING, DevicePlanet, Sweep
-    from fantoch_amd.dist import shard_of, sharded_sweep
+    from fantoch_amd.dist import shard_of, sharded_sweep, world_census
     from fantoch_amd.planet import Planet
 
     wl = workloads()[args.workload]
     planet = Planet.new() if wl["R"] is None else Planet.synthetic(wl["R"])
     n = wl["n"]
-    dp = DevicePlanet(planet, local)
+    dp = DevicePlanet(planet, dev_index)
     srv = np.arange(planet.R, dtype=np.uint32)
     # digest=True: every config's 10 histogram moments and leader feed a
     # checksum, so none of compute_stats' work can be skipped.
@@ -200,8 +233,16 @@ def main():
     kern_ms, launches = sweep.timing()
     tmax = torch.tensor([dt, kern_ms / max(launches, 1)], dtype=torch.float64, device="cuda")
     if world > 1:
-        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+        if rehearsal:
+            tcpu = tmax.cpu()
+            dist.all_reduce(tcpu, op=dist.ReduceOp.MAX)
+            tmax = tcpu
+        else:
+            dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
     dt, kavg_ms = float(tmax[0]), float(tmax[1])
+    census = world_census()
+    if census["ranks"] != list(range(world)):
+        sys.exit(f"bench.py rank {rank}: the collective saw ranks {census['ranks']}, expected 0..{world - 1}")
 
     # the result must equal the oracle-pinned full sweep (every rank holds the merged result)
     fx = load_fixture(args.workload)
@@ -234,7 +275,7 @@ def main():
             "metric": METRIC if args.workload == "r64n7" else f"region configs evaluated/sec, {wl['desc']}",
             "value": total * args.steps / dt,
             "unit": "configs/s",
-            "n_gpus": world,
+            "n_gpus": world if not rehearsal else census["distinct_devices"],
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": dt / args.steps * 1e3,
@@ -253,9 +294,12 @@ def main():
                          "survey_w": W, "survey_w_frac": shard * W / (kavg_ms * 1e-3) / 1e12 / VALU_PEAK_TOPS,
                          "valu_issue": valu, "kernel_ms_avg": kavg_ms,
                          "kernel": KERNEL_NAMES[sweep.kernel_path()]},
+            "world": dict(census, size=world, shard=[b, e]),
             "result_check": {"valid": res.valid, "digest": res.digest, "deferred": sweep.deferred(stream),
                              "top_score_rank": res.tops[0][0][1] if res.tops[0] else None, "fixture": check},
         }
+        if rehearsal:
+            out["rehearsal"] = f"{world} ranks on {census['distinct_devices']} GPU(s) over gloo: not a bench line"
         if os.environ.get("BOTE_LIB_PATH"):
             out["config"]["lib_path"] = os.environ["BOTE_LIB_PATH"]  # an A/B build, not the product library
         if world == 1 and not args.no_cpu_baseline:

@@ -39,6 +39,7 @@ EXPORTS = [
     "bote_sweep_result_device", "bote_merge_device", "bote_sweep_last_kernel_ms",
     "bote_sweep_destroy", "bote_colex_unrank", "bote_binomial", "bote_sweep_timing_reset",
     "bote_sweep_timing", "bote_sweep_grid", "bote_sweep_is_fast", "bote_sweep_split", "bote_sweep_create_ex", "bote_search_topk", "bote_sweep_deferred", "bote_eval_leaderless", "bote_evolving_chains",
+    "bote_search_create", "bote_search_launch", "bote_search_result", "bote_search_bounds", "bote_search_destroy",
 ]
 KERNELS = {None: 0, "auto": 0, "generic": 1, "fast": 2, "group": 3}
 
@@ -123,6 +124,13 @@ def lib():
                                    C.c_uint64, C.c_uint64, C.POINTER(Objective), C.c_uint32, C.c_uint32,
                                    C.POINTER(RankingParamsC), C.c_int, C.POINTER(TopKRecord), _vp,
                                    C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
+    L.bote_search_create.argtypes = [C.POINTER(_vp), C.c_uint32, _u32p, C.c_uint32, _u32p, C.c_uint32, C.c_uint32,
+                                     C.c_uint64, C.c_uint64, C.POINTER(Objective), C.c_uint32, C.c_uint32,
+                                     C.POINTER(RankingParamsC), C.c_int, C.POINTER(_vp)]
+    L.bote_search_launch.argtypes = [_vp]
+    L.bote_search_result.argtypes = [_vp, C.POINTER(TopKRecord), _vp, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
+    L.bote_search_bounds.argtypes = [_vp, C.POINTER(C.c_uint64)]
+    L.bote_search_destroy.argtypes = [_vp]
     L.bote_sweep_launch.argtypes = [_vp, C.c_uint64, C.c_uint64, _vp]
     L.bote_sweep_result.argtypes = [_vp, _vp, C.POINTER(TopKRecord), _vp, C.POINTER(C.c_uint64),
                                     C.POINTER(C.c_uint64)]

@@ -345,6 +345,7 @@ class Search:
     """search.rs:41-512 — exhaustive search, computed on the GPU."""
 
     BATCH = 1 << 18
+    CHAIN_FETCH = 1 << 16  # chains fetched with the count in one device call (evolving_chain_arrays)
 
     def __init__(self, min_n: int, max_n: int, search_input: SearchInput, save_search: bool = False,
                  lat_dir: Optional[str] = None, device: int = 0, planet: Optional[Planet] = None):
@@ -546,16 +547,25 @@ class Search:
             scores = (f64p * 6)(*[x[1].ctypes.data_as(f64p) for x in arrs])
             means = (f64p * 6)(*[x[2].ctypes.data_as(f64p) for x in arrs])
             total = C.c_uint64()
+            # one device chain search per set: fetch up to `cap` chains with the
+            # count; only a set with more chains than the first cap (no limit
+            # given) runs the search again, sized exactly
+            cap = limit if limit is not None else self.CHAIN_FETCH
+            out_idx = np.zeros((cap, 6), np.uint32)
+            out_sc = np.zeros(cap, np.float64)
             check(lib().bote_evolving_chains(self.dp.device, ns, counts, masks, scores, means,
-                                             float(p.min_mean_decrease), int(p.ft_metric.value), 0, None, None,
+                                             float(p.min_mean_decrease), int(p.ft_metric.value), cap,
+                                             ptr(out_idx) if cap else None, ptr(out_sc) if cap else None,
                                              C.byref(total)))
-            nout = total.value if limit is None else min(limit, total.value)
-            out_idx = np.zeros((nout, 6), np.uint32)
-            out_sc = np.zeros(nout, np.float64)
-            if nout:
+            if limit is None and total.value > cap:
+                cap = total.value
+                out_idx = np.zeros((cap, 6), np.uint32)
+                out_sc = np.zeros(cap, np.float64)
                 check(lib().bote_evolving_chains(self.dp.device, ns, counts, masks, scores, means,
-                                                 float(p.min_mean_decrease), int(p.ft_metric.value), nout,
+                                                 float(p.min_mean_decrease), int(p.ft_metric.value), cap,
                                                  ptr(out_idx), ptr(out_sc), C.byref(total)))
+            nout = min(cap, total.value)
+            out_idx, out_sc = out_idx[:nout], out_sc[:nout]
             idx = np.stack([keep[lvl][out_idx[:, lvl]] for lvl in range(6)], axis=1) if nout else \
                 np.zeros((0, 6), np.int64)
             out.append({"ci": ci, "total": total.value, "idx": idx, "score": out_sc})
@@ -812,7 +822,7 @@ class Sweep:
         parts + 1 ascending ranks from rank_begin to rank_end."""
         cache = self.__dict__.setdefault("_splits", {})
         key = (rank_begin, rank_end, parts)
-        if key not in cache:  # (a host walk of the groups: ms at R=64 n=7)
+        if key not in cache:  # (a host walk of the groups, cached in the library too: ~15 ms at R=64 n=7)
             out = (C.c_uint64 * (parts + 1))()
             check(lib().bote_sweep_split(self.h, rank_begin, rank_end, parts, out))
             cache[key] = [int(x) for x in out]
@@ -826,6 +836,56 @@ class Sweep:
     def config_of(self, rank: int) -> List[int]:
         pos = _lib.colex_unrank(rank, self.n, len(self.servers))
         return [int(self.servers[p]) for p in pos]
+
+
+class MultiDeviceSearch:
+    """bote_search_*: the sweep sharded over `planets` (one per shard; the same
+    device may appear more than once), merged on planets[0]'s device, without
+    torch.distributed.  All host work (shard bounds of equal estimated cost and
+    every shard's work-chunk table, from one walk of the rank space) happens
+    here, once; `launch` is device work only and can be repeated."""
+
+    def __init__(self, planets: Sequence[DevicePlanet], servers: Sequence[int], clients: Sequence[int], n: int,
+                 objectives=DEFAULT_OBJECTIVES, K: int = 100, ranking: Optional[RankingParams] = DEFAULT_RANKING,
+                 digest: bool = True, rank_begin: int = 0, rank_end: Optional[int] = None):
+        srv, cli = u32(servers), u32(clients)
+        self.objectives, self.K, self.n_shards = list(objectives), K, len(planets)
+        no = len(self.objectives)
+        objs = (_lib.Objective * max(no, 1))(*[_lib.Objective(k, s) for k, s in self.objectives])
+        rp = C.byref(_lib.ranking_params_c(ranking)) if ranking is not None else None
+        hs = (C.c_void_p * len(planets))(*[p.h.value for p in planets])
+        self._planets = list(planets)  # the handle borrows them
+        self.rank_begin = rank_begin
+        self.rank_end = _lib.binomial(len(srv), n) if rank_end is None else rank_end
+        h = C.c_void_p()
+        check(lib().bote_search_create(hs, len(planets), srv, len(srv), cli, len(cli), n, rank_begin, self.rank_end,
+                                       objs, no, K, rp, 1 if digest else 0, C.byref(h)))
+        self.h = h
+
+    def __del__(self):
+        try:
+            if self.h:
+                lib().bote_search_destroy(self.h)
+                self.h = None
+        except Exception:
+            pass
+
+    def bounds(self) -> List[int]:
+        out = (C.c_uint64 * (self.n_shards + 1))()
+        check(lib().bote_search_bounds(self.h, out))
+        return [int(x) for x in out]
+
+    def launch(self):
+        check(lib().bote_search_launch(self.h))
+
+    def result(self) -> SweepResult:
+        no, K = len(self.objectives), self.K
+        recs = (_lib.TopKRecord * max(no * K, 1))()
+        cnt = np.zeros(max(no, 1), np.uint32)
+        valid, dig = C.c_uint64(), C.c_uint64()
+        check(lib().bote_search_result(self.h, recs, ptr(cnt), C.byref(valid), C.byref(dig)))
+        tops = [[(recs[o * K + i].key, recs[o * K + i].rank) for i in range(cnt[o])] for o in range(no)]
+        return SweepResult(tops, valid.value, dig.value)
 
 
 def search_topk(planets: Sequence[DevicePlanet], servers: Sequence[int], clients: Sequence[int], n: int,

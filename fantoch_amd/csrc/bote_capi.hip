@@ -16,11 +16,14 @@
 #include <vector>
 
 #include "../../include/bote_hip.h"
+#include "bote_host.hpp"
 #include "bote_kernels.hpp"
 
 using bote::EvalArgs;
 using bote::Rec;
 using bote::SingleArgs;
+
+using namespace bote::host;
 
 namespace {
 
@@ -53,32 +56,20 @@ struct DBuf {
   }
   hipError_t reserve(size_t bytes) {
     if (bytes <= cap && p) return hipSuccess;
+    const size_t old = cap;  // grow geometrically: a slightly larger call does not reallocate again
     if (p) (void)hipFree(p);
     p = nullptr;
     cap = 0;
-    return alloc(std::max(bytes, 2 * cap));
+    return alloc(std::max(bytes, 2 * old));
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
   }
   template <class T>
   T* as() const { return (T*)p; }
 };
-
-uint64_t binom_u64(uint32_t m, uint32_t k) {
-  if (k > m) return 0;
-  k = std::min(k, m - k);
-  unsigned __int128 r = 1;
-  for (uint32_t i = 1; i <= k; ++i) {
-    r = r * (m - k + i) / i;
-    if (r > (unsigned __int128)UINT64_MAX) return 0;
-  }
-  return (uint64_t)r;
-}
-
-std::vector<uint64_t> binom_table(uint32_t ns, uint32_t n) {
-  std::vector<uint64_t> t((size_t)(ns + 1) * (n + 1), 0);
-  for (uint32_t m = 0; m <= ns; ++m)
-    for (uint32_t k = 0; k <= n; ++k) t[(size_t)m * (n + 1) + k] = binom_u64(m, k);
-  return t;
-}
 
 int check_regions(const uint32_t* ids, uint32_t n, uint32_t R, bool distinct, const char* what) {
   if (n && !ids) return fail(BOTE_E_ARG, std::string(what) + " is null");
@@ -152,6 +143,7 @@ struct bote_sweep {
   size_t fshm = 0;
   uint32_t xgrid = 0;  // generic fixup grid (deferred configs)
   DBuf cqt, rqt, queue, qcount, lowtab;
+  DBuf dbg;  // BOTE_DEBUG builds: device-assert flag bits
   // group kernel work chunks per launch range (cached: a bench or a shard
   // re-launches the same range), plus the ticket counter
   struct Chunks {
@@ -160,6 +152,10 @@ struct bote_sweep {
     uint32_t n = 0;
   };
   std::map<std::pair<uint64_t, uint64_t>, std::unique_ptr<Chunks>> chunks;
+  // host walks of the groups (bote_host.hpp): one walk serves the split and
+  // the chunk tables of every sub-range it covers (bote_search_* shares one
+  // walk across its shards' sweeps)
+  mutable std::vector<std::shared_ptr<const GroupWalk>> walks;
   DBuf wctr;
   uint64_t last_rb = 0, last_re = 0;
   hipStream_t last_stream = nullptr;
@@ -169,139 +165,9 @@ struct bote_sweep {
 namespace {
 constexpr uint64_t QUEUE_CAP = 1ull << 20;  // deferred near-tie configs per launch
 
-// The fast path's preconditions (bote_sweep.hip header).
-bool fast_eligible(const bote_planet* p, const uint32_t* servers, uint32_t ns, uint32_t nc,
-                   const bote_ranking_params* rp) {
-  if (nc < 2) return false;
-  if (!std::is_sorted(servers, servers + ns)) return false;
-  if (rp && rp->min_fairness_fpaxos_improv != 0.0) return false;
-  for (size_t i = 0; i < p->lat.size(); ++i)
-    if (p->lat[i] > 4095) return false;
-  for (uint32_t i = 0; i < ns; ++i)
-    for (uint32_t j = 0; j < ns; ++j) {
-      uint16_t v = p->lat[(size_t)servers[i] * p->R + servers[j]];
-      if (i == j ? v != 0 : v == 0) return false;
-    }
-  return true;
-}
-
-// Column-major packed-u16 quad layout: col t, quad g, lane i = row rows[4g+i].
-std::vector<uint16_t> quad_layout(const bote_planet* p, const uint32_t* rows, uint32_t nrows, uint32_t& quads) {
-  quads = (nrows + 3) / 4;
-  const uint32_t stride = (quads + 1) * 4;  // u16 per column (one pad slot)
-  std::vector<uint16_t> m((size_t)p->R * stride, 0);
-  for (uint32_t t = 0; t < p->R; ++t)
-    for (uint32_t c = 0; c < nrows; ++c)
-      m[(size_t)t * stride + c] = (uint16_t)(p->lat[(size_t)rows[c] * p->R + t] << bote::LAT_SHIFT);
-  return m;
-}
-// Expected lane utilisation of the group kernel over the whole rank space:
-// groups with smallest fixed position k hold C(k, 3) configs and run in
-// ceil(C(k, 3) / 64) wavefront steps (bote_group.hip).
-double group_utilisation(uint32_t ns, uint32_t n) {
-  const uint32_t F = n - 3;
-  long double cfg = 0, steps = 0;
-  for (uint32_t k = 3; k + F <= ns; ++k) {
-    const long double groups = (long double)binom_u64(ns - 1 - k, F - 1);
-    const uint64_t g = binom_u64(k, 3);
-    cfg += groups * g;
-    steps += groups * (long double)((g + 63) / 64);
-  }
-  return steps > 0 ? (double)(cfg / (64 * steps)) : 0.0;
-}
-
-// Cost-balanced work chunks of [rb, re) for the group kernel
-// (FastArgs::wchunks).  Groups are walked in rank order: a group of C(q0, 3)
-// configs (q0 = its smallest fixed position) contributes ceil(part / 64)
-// wavefront steps plus GROUP_COST steps of per-group precompute for the part
-// of it inside the range.  Returns nchunks + 1 boundaries, or nothing when the
-// range has too many groups to walk (the kernel then splits ranks evenly).
-#ifndef BOTE_GROUP_COST
-#define BOTE_GROUP_COST 0.0  // 0: fitted per client count (group_cost)
-#endif
 #ifndef BOTE_CHUNKS_PER_WAVE
 #define BOTE_CHUNKS_PER_WAVE 32
 #endif
-// One group's precompute in wavefront steps, least-squares fitted to the
-// per-shard kernel times of scripts/shard_balance.py (profiles/r02h_*): 0.64
-// at 64 clients (n=7), 3.7 at 128 clients (n=6); interpolated as a power of
-// the client count in between and clamped outside.
-double group_cost(uint32_t nc) {
-  if (BOTE_GROUP_COST > 0) return BOTE_GROUP_COST;
-  const double c = 0.64 * std::pow((double)nc / 64.0, 2.53);
-  return std::min(8.0, std::max(0.25, c));
-}
-constexpr uint64_t MAX_WALK_GROUPS = 40000000;
-std::vector<uint64_t> group_chunks(uint32_t ns, uint32_t n, uint32_t nc, uint64_t rb, uint64_t re, uint32_t nchunks) {
-  std::vector<uint64_t> out;
-  if (re <= rb || n < 4 || nchunks == 0) return out;
-  const double GROUP_COST = group_cost(nc);
-  const uint32_t F = n - 3;
-  // too many groups to walk (each group holds at least one config): leave
-  // the range to the even split rather than stall the host
-  const uint64_t all_groups = binom_u64(ns - 3, F);
-  if ((all_groups == 0 || all_groups > MAX_WALK_GROUPS) && re - rb > MAX_WALK_GROUPS) return out;
-  // colex unrank of rb: p[j] = the largest m with C(m, j + 1) <= rest
-  std::vector<uint32_t> p(n);
-  uint64_t rest = rb;
-  uint32_t hi = ns;
-  for (int j = (int)n - 1; j >= 0; --j) {
-    uint32_t m = (uint32_t)j;
-    while (m + 1 < hi && binom_u64(m + 1, j + 1) <= rest) ++m;
-    p[j] = m;
-    rest -= binom_u64(m, j + 1);
-    hi = m;
-  }
-  std::vector<uint32_t> q(p.begin() + 3, p.end());
-  std::vector<uint64_t> gb, gl;  // group parts inside the range: start, length
-  std::vector<double> gc;
-  double total = 0;
-  for (;;) {
-    uint64_t base = 0;
-    for (uint32_t k = 0; k < F; ++k) base += binom_u64(q[k], k + 4);
-    const uint64_t g = binom_u64(q[0], 3);
-    const uint64_t b = std::max(base, rb), e = std::min(base + g, re);
-    if (b >= re) break;
-    if (e > b) {
-      const double c = (double)((e - b + 63) / 64) + GROUP_COST;
-      gb.push_back(b);
-      gl.push_back(e - b);
-      gc.push_back(c);
-      total += c;
-      if (gb.size() > MAX_WALK_GROUPS) return out;
-    }
-    if (e >= re) break;
-    // colex successor of the fixed positions (a combination of {3 .. ns-1})
-    uint32_t k = 0;
-    while (k < F && q[k] + 1 >= (k + 1 < F ? q[k + 1] : ns)) ++k;
-    if (k == F) break;
-    ++q[k];
-    for (uint32_t j = 0; j < k; ++j) q[j] = 3 + j;
-  }
-  out.reserve(nchunks + 1);
-  out.push_back(rb);
-  double cum = 0;
-  size_t i = 0;
-  for (uint32_t c = 1; c < nchunks; ++c) {
-    const double tgt = total * c / nchunks;
-    while (i < gc.size() && cum + gc[i] <= tgt) cum += gc[i++];
-    uint64_t bnd = re;
-    if (i < gc.size()) bnd = gb[i] + (uint64_t)((tgt - cum) / gc[i] * (double)gl[i]);
-    out.push_back(std::max(out.back(), std::min(bnd, re)));
-  }
-  out.push_back(re);
-  return out;
-}
-
-// Packed (p0 | p1 << 8 | p2 << 16) 3-subsets of [0, m) in colex order.
-std::vector<uint32_t> low_table(uint32_t m) {
-  std::vector<uint32_t> t;
-  t.reserve(binom_u64(m, 3));
-  for (uint32_t p2 = 2; p2 < m; ++p2)
-    for (uint32_t p1 = 1; p1 < p2; ++p1)
-      for (uint32_t p0 = 0; p0 < p1; ++p0) t.push_back(p0 | (p1 << 8) | (p2 << 16));
-  return t;
-}
 }  // namespace
 
 extern "C" {
@@ -381,17 +247,7 @@ uint64_t bote_binomial(uint32_t ns, uint32_t n) { return binom_u64(ns, n); }
 
 int bote_colex_unrank(uint64_t rank, uint32_t n, uint32_t ns, uint32_t* out) {
   if (!out || n > ns) return fail(BOTE_E_ARG, "bad unrank arguments");
-  uint64_t total = binom_u64(ns, n);
-  if (rank >= total) return fail(BOTE_E_ARG, "rank out of range");
-  uint64_t r = rank;
-  uint32_t hi = ns;
-  for (int j = (int)n - 1; j >= 0; --j) {
-    uint32_t k = j + 1, x = hi - 1;
-    while (x > (uint32_t)j && binom_u64(x, k) > r) --x;
-    out[j] = x;
-    r -= binom_u64(x, k);
-    hi = x;
-  }
+  if (!colex_unrank(rank, n, ns, out)) return fail(BOTE_E_ARG, "rank out of range");
   return BOTE_OK;
 }
 
@@ -811,7 +667,8 @@ int bote_sweep_create_ex(const bote_planet* p, const uint32_t* servers, uint32_t
   // ---- fast path: quad layouts, column sums are computed on the device.
   // `kernel` forces a path (tests, A/B timing; every path is exact); AUTO:
   // the group kernel when eligible and >= 90 % lane utilisation.
-  s->fast = fast_eligible(p, servers, ns, nc, has_score ? rp : nullptr) && kernel != BOTE_KERNEL_GENERIC;
+  const bool fair = has_score && rp && rp->min_fairness_fpaxos_improv != 0.0;
+  s->fast = fast_eligible(p->lat.data(), p->R, servers, ns, nc, fair) && kernel != BOTE_KERNEL_GENERIC;
   if (kernel != BOTE_KERNEL_AUTO && kernel != BOTE_KERNEL_GENERIC && !s->fast)
     return cleanup(fail(BOTE_E_ARG, "the fast/group kernel is not eligible for this planet and lists"));
   if (s->fast) {
@@ -821,9 +678,9 @@ int bote_sweep_create_ex(const bote_planet* p, const uint32_t* servers, uint32_t
     for (uint32_t i = 0; i < p->R; ++i) ident[i] = i;
     bool cli_ident = nc == p->R && std::equal(clients, clients + nc, ident.begin());
     uint32_t cq_quads = 0, rq_quads = 0;
-    auto cq = quad_layout(p, clients, nc, cq_quads);
+    auto cq = quad_layout(p->lat.data(), p->R, clients, nc, bote::LAT_SHIFT, cq_quads);
     std::vector<uint16_t> rq;
-    if (!cli_ident) rq = quad_layout(p, ident.data(), p->R, rq_quads);
+    if (!cli_ident) rq = quad_layout(p->lat.data(), p->R, ident.data(), p->R, bote::LAT_SHIFT, rq_quads);
     if (s->cqt.alloc(cq.size() * 2) != hipSuccess || (!cli_ident && s->rqt.alloc(rq.size() * 2) != hipSuccess) ||
         s->queue.alloc(QUEUE_CAP * 8) != hipSuccess || s->qcount.alloc(16) != hipSuccess)
       return cleanup(fail(BOTE_E_NOMEM, "hipMalloc fast-path buffers"));
@@ -877,6 +734,11 @@ int bote_sweep_create_ex(const bote_planet* p, const uint32_t* servers, uint32_t
     f.queue = s->queue.as<uint64_t>();
     f.queue_count = s->qcount.as<unsigned long long>();
     f.queue_cap = QUEUE_CAP;
+#ifdef BOTE_DEBUG
+    if (s->dbg.alloc(16) != hipSuccess || hipMemset(s->dbg.p, 0, 16) != hipSuccess)
+      return cleanup(fail(BOTE_E_NOMEM, "debug flag"));
+    f.dbg_flag = s->dbg.as<unsigned int>();
+#endif
 #ifdef BOTE_ABLATION
     const char* abl = getenv("BOTE_ABLATE");  // timing-diagnostics builds only
     f.ablate = abl ? (uint32_t)strtoul(abl, nullptr, 0) : 0u;
@@ -898,6 +760,9 @@ int bote_sweep_create_ex(const bote_planet* p, const uint32_t* servers, uint32_t
       if (!lt.empty() && hipMemcpy(s->lowtab.p, lt.data(), lt.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
         return cleanup(fail(BOTE_E_DEVICE, "upload group low table"));
       f.lowtab = s->lowtab.as<uint32_t>();
+#ifdef BOTE_DEBUG
+      f.lowtab_n = lt.size();
+#endif
       // workgroup size: 256 threads (4 waves).  Larger workgroups (which
       // share the client-quad matrix, so R = 128 fits more waves per CU) were
       // measured slower: R=128 n=6 at 640 threads, 5 waves/SIMD, 369 ms vs
@@ -905,8 +770,12 @@ int bote_sweep_create_ex(const bote_planet* p, const uint32_t* servers, uint32_t
 #ifndef BOTE_GROUP_BD
 #define BOTE_GROUP_BD 256
 #endif
+      static_assert(BOTE_GROUP_BD % 64 == 0 && BOTE_GROUP_BD <= 1024, "group workgroup: 64..1024 threads");
       f.gbd = BOTE_GROUP_BD;
+      // qtab member planes (non-PERM kernels): one u32 per thread, so the
+      // plane stride 1 << gqsh must hold gbd * 4 bytes (bote_group.hip)
       f.gqsh = 10;
+      while ((1u << f.gqsh) < f.gbd * 4) ++f.gqsh;
       f.gslots = 0;
       f.grx = 0;
       // bote.py DEFAULT_OBJECTIVES: SCORE, MEAN af1, MEAN ff1, COV af1, MEAN e
@@ -919,17 +788,17 @@ int bote_sweep_create_ex(const bote_planet* p, const uint32_t* servers, uint32_t
         // the per-group position table (n <= 7) unless its LDS lowers the
         // workgroups per CU (R = 64: 4 either way, register-bound; R = 128:
         // 3 without, 2 with it, measured 255 vs 280 ms)
-        const int occ_plain = bote::group_occupancy(n, bote::group_smem_bytes(f, n), s->def_obj, f.gbd);
+        const int occ_plain = bote::group_occupancy(f, n, bote::group_smem_bytes(f, n), s->def_obj);
         f.grx = 1;
-        if (bote::group_occupancy(n, bote::group_smem_bytes(f, n), s->def_obj, f.gbd) < occ_plain) f.grx = 0;
+        if (bote::group_occupancy(f, n, bote::group_smem_bytes(f, n), s->def_obj) < occ_plain) f.grx = 0;
         // client lines per wave: as many (<= 16) as keep the workgroups per
         // CU of the kernel without lines (a step has 7.7 distinct (p1, p2)
         // on average at R=64 n=7, 4.0 at R=128 n=6)
-        const int occ0 = bote::group_occupancy(n, bote::group_smem_bytes(f, n), s->def_obj, f.gbd);
+        const int occ0 = bote::group_occupancy(f, n, bote::group_smem_bytes(f, n), s->def_obj);
         for (uint32_t sl = 16; sl >= 1; --sl) {
           f.gslots = sl;
           const size_t sh = bote::group_smem_bytes(f, n);
-          if (sh <= device_max_lds(p->device) && bote::group_occupancy(n, sh, s->def_obj, f.gbd) >= occ0) break;
+          if (sh <= device_max_lds(p->device) && bote::group_occupancy(f, n, sh, s->def_obj) >= occ0) break;
           f.gslots = 0;
         }
       }
@@ -937,7 +806,7 @@ int bote_sweep_create_ex(const bote_planet* p, const uint32_t* servers, uint32_t
       if (gshm <= device_max_lds(p->device)) {
         s->group = true;
         s->fshm = gshm;
-        s->fgrid = (uint32_t)(device_cus(p->device) * std::max(1, bote::group_occupancy(n, gshm, s->def_obj, f.gbd)));
+        s->fgrid = (uint32_t)(device_cus(p->device) * std::max(1, bote::group_occupancy(f, n, gshm, s->def_obj)));
       }
     }
   }
@@ -965,20 +834,65 @@ int bote_sweep_is_fast(const bote_sweep* s, int* out) {
   return BOTE_OK;
 }
 
+// The cached group walk covering [rb, re) (walked on first use; a handful of
+// walks are kept, the oldest dropped first).  Null off the group kernel or
+// when the range has too many groups to walk.
+static std::shared_ptr<const GroupWalk> walk_for(const bote_sweep* s, uint64_t rb, uint64_t re) {
+  if (!s->fast || !s->group || re <= rb) return nullptr;
+  for (const auto& w : s->walks)
+    if (w->covers(rb, re)) return w;
+  std::shared_ptr<const GroupWalk> w = walk_groups(s->ns, s->n, s->nc, rb, re);
+  if (!w) return nullptr;
+  if (s->walks.size() >= 8) s->walks.erase(s->walks.begin());
+  s->walks.push_back(w);
+  return w;
+}
+
 int bote_sweep_split(const bote_sweep* s, uint64_t rank_begin, uint64_t rank_end, uint32_t parts,
                      uint64_t* out_bounds) {
   if (!s || !out_bounds) return fail(BOTE_E_ARG, "null argument");
   if (parts == 0) return fail(BOTE_E_ARG, "parts must be >= 1");
   if (rank_begin > rank_end || rank_end > binom_u64(s->ns, s->n)) return fail(BOTE_E_ARG, "rank range out of bounds");
   std::vector<uint64_t> b;
-  if (s->fast && s->group && rank_end - rank_begin >= (uint64_t)parts * 64)
-    b = group_chunks(s->ns, s->n, s->nc, rank_begin, rank_end, parts);
+  if (rank_end - rank_begin >= (uint64_t)parts * 64) {
+    if (auto w = walk_for(s, rank_begin, rank_end)) b = cut_chunks(*w, rank_begin, rank_end, parts);
+  }
   if (b.size() != (size_t)parts + 1) {
     b.resize((size_t)parts + 1);
     const uint64_t span = rank_end - rank_begin;
     for (uint32_t i = 0; i <= parts; ++i) b[i] = rank_begin + (uint64_t)(((unsigned __int128)span * i) / parts);
   }
   std::copy(b.begin(), b.end(), out_bounds);
+  return BOTE_OK;
+}
+
+// The group kernel's work-chunk table for [rb, re): cut from a cached walk
+// and uploaded on `st` once per range (a bench or a shard re-launches the same
+// range).  Null chunks (even rank split in the kernel) off the group kernel.
+static int sweep_chunks(bote_sweep* s, uint64_t rb, uint64_t re, hipStream_t st, const bote_sweep::Chunks** out) {
+  *out = nullptr;
+  if (!s->fast || !s->group) return BOTE_OK;
+  auto key = std::make_pair(rb, re);
+  auto it = s->chunks.find(key);
+  if (it == s->chunks.end()) {
+    if (s->chunks.size() >= 16) {  // bounded cache: drain the last stream before freeing
+      if (s->last_stream) HIP_TRY(hipStreamSynchronize(s->last_stream));
+      HIP_TRY(hipStreamSynchronize(st));
+      s->chunks.clear();
+    }
+    auto c = std::make_unique<bote_sweep::Chunks>();
+    const uint32_t nwaves = s->fgrid * (s->fargs.gbd / 64);
+    // (no chunk below ~4 wavefront steps of configs)
+    const uint64_t want = std::min<uint64_t>((uint64_t)nwaves * BOTE_CHUNKS_PER_WAVE, (re - rb) / 256 + 1);
+    if (auto w = walk_for(s, rb, re)) c->host = cut_chunks(*w, rb, re, (uint32_t)want);
+    if (!c->host.empty()) {
+      c->n = (uint32_t)c->host.size() - 1;
+      if (c->dev.alloc(c->host.size() * 8) != hipSuccess) return fail(BOTE_E_NOMEM, "hipMalloc work chunks");
+      HIP_TRY(hipMemcpyAsync(c->dev.p, c->host.data(), c->host.size() * 8, hipMemcpyHostToDevice, st));
+    }
+    it = s->chunks.emplace(key, std::move(c)).first;
+  }
+  *out = it->second.get();
   return BOTE_OK;
 }
 
@@ -1065,28 +979,11 @@ static int launch_fast_path(bote_sweep* s, uint64_t rb, uint64_t re, hipStream_t
   HIP_TRY(hipMemsetAsync(s->qcount.p, 0, 8, st));
   if (s->group) {
     // cost-balanced chunks (32 per wave), taken dynamically (bote_group.hip)
-    auto key = std::make_pair(rb, re);
-    auto it = s->chunks.find(key);
-    if (it == s->chunks.end()) {
-      if (s->chunks.size() >= 16) {  // bounded cache: drain the last stream before freeing
-        if (s->last_stream) HIP_TRY(hipStreamSynchronize(s->last_stream));
-        HIP_TRY(hipStreamSynchronize(st));
-        s->chunks.clear();
-      }
-      auto c = std::make_unique<bote_sweep::Chunks>();
-      const uint32_t nwaves = s->fgrid * (f.gbd / 64);
-      // (no chunk below ~4 wavefront steps of configs)
-      const uint64_t want = std::min<uint64_t>((uint64_t)nwaves * BOTE_CHUNKS_PER_WAVE, (re - rb) / 256 + 1);
-      c->host = group_chunks(s->ns, s->n, s->nc, rb, re, (uint32_t)want);
-      if (!c->host.empty()) {
-        c->n = (uint32_t)c->host.size() - 1;
-        if (c->dev.alloc(c->host.size() * 8) != hipSuccess) return fail(BOTE_E_NOMEM, "hipMalloc work chunks");
-        HIP_TRY(hipMemcpyAsync(c->dev.p, c->host.data(), c->host.size() * 8, hipMemcpyHostToDevice, st));
-      }
-      it = s->chunks.emplace(key, std::move(c)).first;
-    }
-    f.nwchunks = it->second->n;
-    f.wchunks = it->second->dev.as<uint64_t>();
+    const bote_sweep::Chunks* ch = nullptr;
+    int crc = sweep_chunks(s, rb, re, st, &ch);
+    if (crc) return crc;
+    f.nwchunks = ch ? ch->n : 0;
+    f.wchunks = ch ? ch->dev.as<uint64_t>() : nullptr;
     if (f.nwchunks) {
       if (!s->wctr.p && s->wctr.alloc(16) != hipSuccess) return fail(BOTE_E_NOMEM, "hipMalloc work counter");
       f.wctr = s->wctr.as<unsigned int>();
@@ -1156,21 +1053,8 @@ int bote_sweep_result_device(bote_sweep* s, void* dst, void* hip_stream) {
 
 static void unpack_result(const bote_sweep* s, const std::vector<uint8_t>& blk, bote_topk_record* out,
                           uint32_t* out_count, uint64_t* out_valid, uint64_t* out_digest) {
-  const Rec* r = (const Rec*)blk.data();
-  for (uint32_t o = 0; o < s->n_obj; ++o) {
-    uint32_t c = 0;
-    for (uint32_t i = 0; i < s->K; ++i) {
-      Rec x = r[(size_t)o * bote::KP + i];
-      if (x.key == ~0ull && x.rank == ~0ull) break;
-      if (out) out[(size_t)o * s->K + i] = bote_topk_record{x.key, x.rank};
-      ++c;
-    }
-    for (uint32_t i = c; out && i < s->K; ++i) out[(size_t)o * s->K + i] = bote_topk_record{~0ull, ~0ull};
-    if (out_count) out_count[o] = c;
-  }
-  const uint64_t* cnt = (const uint64_t*)(blk.data() + (size_t)s->n_obj * bote::KP * 16);
-  if (out_valid) *out_valid = cnt[0];
-  if (out_digest) *out_digest = cnt[1];
+  static_assert(sizeof(bote_topk_record) == sizeof(TopkRecord), "record layout");
+  bote::host::unpack_result(blk.data(), s->n_obj, s->K, bote::KP, (TopkRecord*)out, out_count, out_valid, out_digest);
 }
 
 int bote_sweep_result(bote_sweep* s, void* hip_stream, bote_topk_record* out, uint32_t* out_count,
@@ -1181,6 +1065,13 @@ int bote_sweep_result(bote_sweep* s, void* hip_stream, bote_topk_record* out, ui
   std::vector<uint8_t> blk(s->result_bytes());
   HIP_TRY(hipMemcpyAsync(blk.data(), s->result.p, blk.size(), hipMemcpyDeviceToHost, (hipStream_t)hip_stream));
   HIP_TRY(hipStreamSynchronize((hipStream_t)hip_stream));
+#ifdef BOTE_DEBUG
+  if (s->dbg.p) {
+    unsigned int flag = 0;
+    HIP_TRY(hipMemcpy(&flag, s->dbg.p, 4, hipMemcpyDeviceToHost));
+    if (flag) return fail(BOTE_E_DEVICE, "device assert failed (BOTE_DEBUG), flag bits " + std::to_string(flag));
+  }
+#endif
   unpack_result(s, blk, out, out_count, out_valid, out_digest);
   return BOTE_OK;
 }
@@ -1262,19 +1153,73 @@ int bote_sweep_destroy(bote_sweep* s) {
 
 
 // ------------------------------------------------- multi-device search ----
-// SURVEY.md §8b bote_search_topk: the whole sharded search in one call, no
-// PyTorch.  Shard i of [rank_begin, rank_end) sweeps on planets[i]'s device on
-// a stream of its own; the per-shard result blocks meet on planets[0]'s device
-// (peer copies), where a deterministic (key, rank) merge tree combines them.
-// The result equals one unsharded sweep (the merge order does not depend on
-// the number of shards).  Reference: the only parallelism of the reference
-// search is rayon over client sets (search.rs:209-231); this is its
-// replacement for one client set over the GPUs of a node.
-int bote_search_topk(const bote_planet* const* planets, uint32_t n_devices, const uint32_t* servers, uint32_t ns,
-                     const uint32_t* clients, uint32_t nc, uint32_t n, uint64_t rank_begin, uint64_t rank_end,
-                     const bote_objective* objs, uint32_t n_obj, uint32_t K, const bote_ranking_params* rp,
-                     int digest, bote_topk_record* out, uint32_t* out_count, uint64_t* out_valid,
-                     uint64_t* out_digest) {
+// the whole sharded search without PyTorch.  A bote_search
+// holds, per shard i of [rank_begin, rank_end), a sweep on planets[i]'s device
+// with a stream of its own, its rank bounds (equal estimated cost: one host
+// walk of the groups, shared by every shard's sweep) and its uploaded
+// work-chunk table; plus the gather and merge buffers on planets[0]'s device.
+// A launch is then device work only: every shard's sweep and merge chain, a
+// peer copy of its result block to the root device, and a deterministic
+// (key, rank) merge tree there.  The result equals one unsharded sweep (the
+// merge order does not depend on the number of shards).  Reference: the only
+// parallelism of the reference search is rayon over client sets
+// (search.rs:209-231); this replaces it for one client set over a node's GPUs.
+struct bote_search {
+  struct Shard {
+    bote_sweep* sw = nullptr;
+    hipStream_t st = nullptr;
+    hipEvent_t done = nullptr;
+    DBuf local;  // the shard's result block on its own device (remote shards)
+    uint64_t b = 0, e = 0;
+    int dev = 0;
+  };
+  std::vector<Shard> sh;
+  int root = 0;
+  hipStream_t rst = nullptr;
+  DBuf gathered, bufa, bufb, merged;
+  uint64_t nb = 0;
+  uint64_t rb = 0, re = 0;
+  bool launched = false;
+};
+
+namespace {
+// Drains every stream of the handle, then frees it (any state, error paths too).
+void search_free(bote_search* h) {
+  if (!h) return;
+  for (auto& x : h->sh) {
+    if (x.st) {
+      (void)hipSetDevice(x.dev);
+      (void)hipStreamSynchronize(x.st);
+    }
+  }
+  if (h->rst) {
+    (void)hipSetDevice(h->root);
+    (void)hipStreamSynchronize(h->rst);
+    (void)hipStreamDestroy(h->rst);
+  }
+  for (auto& x : h->sh) {
+    (void)hipSetDevice(x.dev);
+    if (x.done) (void)hipEventDestroy(x.done);
+    if (x.st) (void)hipStreamDestroy(x.st);
+    if (x.sw) bote_sweep_destroy(x.sw);
+    x.local.release();
+  }
+  (void)hipSetDevice(h->root);
+  delete h;
+}
+
+// hipError_t -> BOTE_E_DEVICE with context (no early return past cleanup)
+int hip_fail(hipError_t e, const char* what) {
+  return fail(BOTE_E_DEVICE, std::string(what) + ": " + hipGetErrorString(e));
+}
+}  // namespace
+
+int bote_search_create(const bote_planet* const* planets, uint32_t n_devices, const uint32_t* servers, uint32_t ns,
+                       const uint32_t* clients, uint32_t nc, uint32_t n, uint64_t rank_begin, uint64_t rank_end,
+                       const bote_objective* objs, uint32_t n_obj, uint32_t K, const bote_ranking_params* rp,
+                       int digest, bote_search** out) {
+  if (!out) return fail(BOTE_E_ARG, "out is null");
+  *out = nullptr;
   if (!planets || n_devices == 0) return fail(BOTE_E_ARG, "no planets");
   if (n_devices > 1024) return fail(BOTE_E_RANGE, "at most 1024 shards");
   for (uint32_t i = 0; i < n_devices; ++i) {
@@ -1282,101 +1227,154 @@ int bote_search_topk(const bote_planet* const* planets, uint32_t n_devices, cons
     if (planets[i]->R != planets[0]->R || planets[i]->lat != planets[0]->lat)
       return fail(BOTE_E_ARG, "the shards' planets differ");
   }
+  if (n > ns) return fail(BOTE_E_ARG, "config size larger than the server list");
   const uint64_t total = binom_u64(ns, n);
   if (rank_begin > rank_end || rank_end > total) return fail(BOTE_E_ARG, "rank range out of bounds");
-  struct Shard {
-    bote_sweep* sw = nullptr;
-    hipStream_t st = nullptr;
-    hipEvent_t done = nullptr;
-    DBuf local;
-  };
-  std::vector<Shard> sh(n_devices);
-  const int root = planets[0]->device;
-  hipStream_t rst = nullptr;
-  DBuf gathered, bufa, bufb, merged;
-  int rc = BOTE_OK;
+  auto* h = new bote_search();
+  h->sh = std::vector<bote_search::Shard>(n_devices);
+  h->root = planets[0]->device;
+  h->rb = rank_begin;
+  h->re = rank_end;
   auto cleanup = [&](int code) {
-    for (auto& x : sh) {
-      if (x.st) {
-        (void)hipSetDevice(x.sw ? x.sw->p->device : root);
-        (void)hipStreamSynchronize(x.st);
-      }
-    }
-    if (rst) {
-      (void)hipSetDevice(root);
-      (void)hipStreamSynchronize(rst);
-      (void)hipStreamDestroy(rst);
-    }
-    for (auto& x : sh) {
-      const int dev = x.sw ? x.sw->p->device : root;
-      (void)hipSetDevice(dev);
-      if (x.done) (void)hipEventDestroy(x.done);
-      if (x.st) (void)hipStreamDestroy(x.st);
-      if (x.sw) bote_sweep_destroy(x.sw);
-    }
+    search_free(h);
     return code;
   };
-  // shards: create, launch (asynchronous, one stream each)
+  hipError_t e;
+  int rc;
   for (uint32_t i = 0; i < n_devices; ++i) {
-    if ((rc = bote_sweep_create(planets[i], servers, ns, clients, nc, n, objs, n_obj, K, rp, digest, &sh[i].sw)))
+    auto& x = h->sh[i];
+    x.dev = planets[i]->device;
+    if ((rc = bote_sweep_create(planets[i], servers, ns, clients, nc, n, objs, n_obj, K, rp, digest, &x.sw)))
       return cleanup(rc);
-    HIP_TRY(hipSetDevice(planets[i]->device));
-    if (hipStreamCreateWithFlags(&sh[i].st, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreateWithFlags(&sh[i].done, hipEventDisableTiming) != hipSuccess)
-      return cleanup(fail(BOTE_E_DEVICE, "shard stream/event"));
+    if ((e = hipSetDevice(x.dev)) != hipSuccess) return cleanup(hip_fail(e, "hipSetDevice (shard)"));
+    if ((e = hipStreamCreateWithFlags(&x.st, hipStreamNonBlocking)) != hipSuccess ||
+        (e = hipEventCreateWithFlags(&x.done, hipEventDisableTiming)) != hipSuccess)
+      return cleanup(hip_fail(e, "shard stream/event"));
   }
-  // shards of equal estimated cost (bote_sweep_split)
+  // shards of equal estimated cost from one walk of the groups, shared by
+  // every shard's sweep (their chunk tables are cut from it)
   std::vector<uint64_t> bnd((size_t)n_devices + 1);
-  if ((rc = bote_sweep_split(sh[0].sw, rank_begin, rank_end, n_devices, bnd.data()))) return cleanup(rc);
-  for (uint32_t i = 0; i < n_devices; ++i)
-    if ((rc = bote_sweep_launch(sh[i].sw, bnd[i], bnd[i + 1], sh[i].st))) return cleanup(rc);
-  // gather on the root device
-  const uint64_t nb = sh[0].sw->result_bytes();
-  if (hipSetDevice(root) != hipSuccess || hipStreamCreateWithFlags(&rst, hipStreamNonBlocking) != hipSuccess ||
-      gathered.alloc(nb * n_devices) != hipSuccess || bufa.alloc(nb * ((n_devices + 7) / 8)) != hipSuccess ||
-      bufb.alloc(nb * ((n_devices + 7) / 8)) != hipSuccess || merged.alloc(nb) != hipSuccess)
-    return cleanup(fail(BOTE_E_NOMEM, "gather buffers"));
+  if ((rc = bote_sweep_split(h->sh[0].sw, rank_begin, rank_end, n_devices, bnd.data()))) return cleanup(rc);
+  for (uint32_t i = 1; i < n_devices; ++i)
+    for (const auto& w : h->sh[0].sw->walks) h->sh[i].sw->walks.push_back(w);
   for (uint32_t i = 0; i < n_devices; ++i) {
-    const int dev = planets[i]->device;
-    char* dst = gathered.as<char>() + nb * i;
-    if (dev == root) {
-      if ((rc = bote_sweep_result_device(sh[i].sw, dst, sh[i].st))) return cleanup(rc);
-    } else {
-      HIP_TRY(hipSetDevice(dev));
-      if (sh[i].local.alloc(nb) != hipSuccess) return cleanup(fail(BOTE_E_NOMEM, "shard result block"));
-      if ((rc = bote_sweep_result_device(sh[i].sw, sh[i].local.p, sh[i].st))) return cleanup(rc);
-      if (hipMemcpyPeerAsync(dst, root, sh[i].local.p, dev, nb, sh[i].st) != hipSuccess)
-        return cleanup(fail(BOTE_E_DEVICE, "peer copy of a shard result"));
-    }
-    (void)hipSetDevice(dev);
-    if (hipEventRecord(sh[i].done, sh[i].st) != hipSuccess) return cleanup(fail(BOTE_E_DEVICE, "record shard event"));
+    auto& x = h->sh[i];
+    x.b = bnd[i];
+    x.e = bnd[i + 1];
+    const bote_sweep::Chunks* ch = nullptr;
+    if ((e = hipSetDevice(x.dev)) != hipSuccess) return cleanup(hip_fail(e, "hipSetDevice (shard)"));
+    if ((rc = sweep_chunks(x.sw, x.b, x.e, x.st, &ch))) return cleanup(rc);
   }
-  HIP_TRY(hipSetDevice(root));
-  for (uint32_t i = 0; i < n_devices; ++i)
-    if (hipStreamWaitEvent(rst, sh[i].done, 0) != hipSuccess) return cleanup(fail(BOTE_E_DEVICE, "wait shard"));
+  // gather + merge buffers on the root device
+  h->nb = h->sh[0].sw->result_bytes();
+  const size_t groups = (n_devices + bote::G_MERGE_LISTS - 1) / bote::G_MERGE_LISTS;
+  if ((e = hipSetDevice(h->root)) != hipSuccess) return cleanup(hip_fail(e, "hipSetDevice (root)"));
+  if ((e = hipStreamCreateWithFlags(&h->rst, hipStreamNonBlocking)) != hipSuccess)
+    return cleanup(hip_fail(e, "root stream"));
+  if (h->gathered.alloc(h->nb * n_devices) != hipSuccess || h->bufa.alloc(h->nb * groups) != hipSuccess ||
+      h->bufb.alloc(h->nb * groups) != hipSuccess || h->merged.alloc(h->nb) != hipSuccess)
+    return cleanup(fail(BOTE_E_NOMEM, "gather buffers"));
+  for (auto& x : h->sh) {
+    if (x.dev == h->root) continue;
+    if ((e = hipSetDevice(x.dev)) != hipSuccess) return cleanup(hip_fail(e, "hipSetDevice (shard)"));
+    if (x.local.alloc(h->nb) != hipSuccess) return cleanup(fail(BOTE_E_NOMEM, "shard result block"));
+  }
+  // the chunk uploads are stream-ordered before the first launch; drain them
+  // here so that create returns with the handle idle
+  for (auto& x : h->sh) {
+    (void)hipSetDevice(x.dev);
+    if ((e = hipStreamSynchronize(x.st)) != hipSuccess) return cleanup(hip_fail(e, "shard setup"));
+  }
+  (void)hipSetDevice(h->root);
+  *out = h;
+  return BOTE_OK;
+}
+
+int bote_search_bounds(const bote_search* h, uint64_t* out_bounds) {
+  if (!h || !out_bounds) return fail(BOTE_E_ARG, "null argument");
+  for (size_t i = 0; i < h->sh.size(); ++i) out_bounds[i] = h->sh[i].b;
+  out_bounds[h->sh.size()] = h->sh.empty() ? h->rb : h->sh.back().e;
+  return BOTE_OK;
+}
+
+int bote_search_launch(bote_search* h) {
+  if (!h) return fail(BOTE_E_ARG, "search is null");
+  int rc;
+  hipError_t e;
+  const uint32_t nd = (uint32_t)h->sh.size();
+  // every shard first (asynchronous, one stream each: no host work between)
+  for (auto& x : h->sh)
+    if ((rc = bote_sweep_launch(x.sw, x.b, x.e, x.st))) return rc;
+  for (uint32_t i = 0; i < nd; ++i) {
+    auto& x = h->sh[i];
+    char* dst = h->gathered.as<char>() + h->nb * i;
+    if (x.dev == h->root) {
+      if ((rc = bote_sweep_result_device(x.sw, dst, x.st))) return rc;
+    } else {
+      if ((rc = bote_sweep_result_device(x.sw, x.local.p, x.st))) return rc;
+      if ((e = hipMemcpyPeerAsync(dst, h->root, x.local.p, x.dev, h->nb, x.st)) != hipSuccess)
+        return hip_fail(e, "peer copy of a shard result");
+    }
+    if ((e = hipSetDevice(x.dev)) != hipSuccess || (e = hipEventRecord(x.done, x.st)) != hipSuccess)
+      return hip_fail(e, "record shard event");
+  }
+  if ((e = hipSetDevice(h->root)) != hipSuccess) return hip_fail(e, "hipSetDevice (root)");
+  for (auto& x : h->sh)
+    if ((e = hipStreamWaitEvent(h->rst, x.done, 0)) != hipSuccess) return hip_fail(e, "wait shard");
   // merge tree, at most 8 blocks per merge
-  const char* src = gathered.as<char>();
-  uint32_t m = n_devices;
-  char* bufs[2] = {bufa.as<char>(), bufb.as<char>()};
+  const char* src = h->gathered.as<char>();
+  uint32_t m = nd;
+  char* bufs[2] = {h->bufa.as<char>(), h->bufb.as<char>()};
   int bsel = 0;
+  const bote_sweep* s0 = h->sh[0].sw;
   while (m > (uint32_t)bote::G_MERGE_LISTS) {
     const uint32_t groups = (m + bote::G_MERGE_LISTS - 1) / bote::G_MERGE_LISTS;
     for (uint32_t g = 0; g < groups; ++g) {
       const uint32_t k = std::min<uint32_t>(bote::G_MERGE_LISTS, m - bote::G_MERGE_LISTS * g);
-      if ((rc = bote_merge_device(sh[0].sw, src + (size_t)nb * bote::G_MERGE_LISTS * g, k, bufs[bsel] + (size_t)nb * g,
-                                  rst)))
-        return cleanup(rc);
+      if ((rc = bote_merge_device(s0, src + (size_t)h->nb * bote::G_MERGE_LISTS * g, k, bufs[bsel] + (size_t)h->nb * g,
+                                  h->rst)))
+        return rc;
     }
     src = bufs[bsel];
     bsel ^= 1;
     m = groups;
   }
-  if ((rc = bote_merge_device(sh[0].sw, src, m, merged.p, rst))) return cleanup(rc);
-  std::vector<uint8_t> blk(nb);
-  HIP_TRY(hipMemcpyAsync(blk.data(), merged.p, nb, hipMemcpyDeviceToHost, rst));
-  HIP_TRY(hipStreamSynchronize(rst));
-  unpack_result(sh[0].sw, blk, out, out_count, out_valid, out_digest);
-  return cleanup(BOTE_OK);
+  if ((rc = bote_merge_device(s0, src, m, h->merged.p, h->rst))) return rc;
+  h->launched = true;
+  return BOTE_OK;
+}
+
+int bote_search_result(bote_search* h, bote_topk_record* out, uint32_t* out_count, uint64_t* out_valid,
+                       uint64_t* out_digest) {
+  if (!h) return fail(BOTE_E_ARG, "search is null");
+  if (!h->launched) return fail(BOTE_E_ARG, "search not launched");
+  HIP_TRY(hipSetDevice(h->root));
+  std::vector<uint8_t> blk(h->nb);
+  HIP_TRY(hipMemcpyAsync(blk.data(), h->merged.p, h->nb, hipMemcpyDeviceToHost, h->rst));
+  HIP_TRY(hipStreamSynchronize(h->rst));
+  unpack_result(h->sh[0].sw, blk, out, out_count, out_valid, out_digest);
+  return BOTE_OK;
+}
+
+int bote_search_destroy(bote_search* h) {
+  search_free(h);
+  return BOTE_OK;
+}
+
+int bote_search_topk(const bote_planet* const* planets, uint32_t n_devices, const uint32_t* servers, uint32_t ns,
+                     const uint32_t* clients, uint32_t nc, uint32_t n, uint64_t rank_begin, uint64_t rank_end,
+                     const bote_objective* objs, uint32_t n_obj, uint32_t K, const bote_ranking_params* rp,
+                     int digest, bote_topk_record* out, uint32_t* out_count, uint64_t* out_valid,
+                     uint64_t* out_digest) {
+  bote_search* h = nullptr;
+  int rc = bote_search_create(planets, n_devices, servers, ns, clients, nc, n, rank_begin, rank_end, objs, n_obj, K,
+                              rp, digest, &h);
+  if (rc) return rc;
+  if (!(rc = bote_search_launch(h))) rc = bote_search_result(h, out, out_count, out_valid, out_digest);
+  const std::string err = g_err;
+  search_free(h);
+  if (rc) g_err = err;
+  return rc;
 }
 
 }  // extern "C"

@@ -436,6 +436,7 @@ __global__ void __launch_bounds__(GROUP_MAX_BD, GCfg<N>::PERM ? BOTE_GROUP_WAVES
     if (c >= a.nwchunks) break;
     r = uni64(a.wchunks[c]);
     rend = uni64(a.wchunks[c + 1]);
+    GASSERT(a, a.rb <= r && r <= rend && rend <= a.re, 0);  // chunk inside the launch range
   } else {
     if (static_done) break;
     static_done = true;
@@ -460,6 +461,13 @@ __global__ void __launch_bounds__(GROUP_MAX_BD, GCfg<N>::PERM ? BOTE_GROUP_WAVES
       base = uni64(base);
     }
     uint64_t low = r - base;
+#ifdef BOTE_DEBUG
+    {
+      bool okq = hq[0] >= 3 && hq[F - 1] < a.ns;
+      for (int k = 1; k < F; ++k) okq = okq && hq[k - 1] < hq[k];
+      GASSERT(a, okq, 1);  // fixed positions: ascending, above the 3 variable ones, < ns
+    }
+#endif
     for (;;) {
       const uint64_t gend = base + uni64(binom[hq[0] * (N + 1) + 3]);
       // ---------------- per-group, wave-uniform precompute -> group line
@@ -509,7 +517,9 @@ __global__ void __launch_bounds__(GROUP_MAX_BD, GCfg<N>::PERM ? BOTE_GROUP_WAVES
         }
         s16(mfl + 2 * c, key);
       }
+      GASSERT(a, PERM || (tid + 1) * 4 <= (1u << qsh), 6);  // qtab plane holds every thread's word
       if (use_rx) {
+        GASSERT(a, hq[0] <= a.ns, 5);  // position table rows (ns x 16 B per wave)
         // positions below the smallest fixed one: sorted distances to the
         // fixed members (row part), the fixed members' distances to x
         // (column part, packed as the fixed-row pairs); absent members INF
@@ -531,6 +541,7 @@ __global__ void __launch_bounds__(GROUP_MAX_BD, GCfg<N>::PERM ? BOTE_GROUP_WAVES
 
       // ---------------- the group's configs, 64 per step
       const uint64_t cend = uni64(gend < rend ? gend : rend);
+      GASSERT(a, low + (cend - r) <= a.lowtab_n, 2);  // low-table rows of the group's configs
       uint32_t lp3 = a.lowtab[low + min((uint64_t)lane, cend - r - 1)];  // prefetched
       while (r < cend) {
         const uint32_t len = (uint32_t)min((uint64_t)64, cend - r);
@@ -566,6 +577,7 @@ __global__ void __launch_bounds__(GROUP_MAX_BD, GCfg<N>::PERM ? BOTE_GROUP_WAVES
             const bool starts = (nk >> lane) & 1;
             const uint32_t slot = below + (starts ? 1u : 0u) - 1;
             ll = lines + slot * cstride;
+            GASSERT(a, !have || slot < a.gslots, 4);  // client-line slot
             if (starts) s32(keys + 4 * slot, cur);
             wave_sync();
             // then lpl lanes per line (one quad = 4 clients each), 64 / lpl
@@ -597,6 +609,7 @@ __global__ void __launch_bounds__(GROUP_MAX_BD, GCfg<N>::PERM ? BOTE_GROUP_WAVES
           pv[0] = cur & 0xFF;
           pv[1] = (cur >> 8) & 0xFF;
           pv[2] = cur >> 16;
+          GASSERT(a, pv[0] < pv[1] && pv[1] < pv[2] && pv[2] < hq[0], 3);  // variable positions below the fixed ones
 #pragma unroll
           for (int i = 0; i < 3; ++i) rv[i] = sid ? pv[i] : srv[pv[i]];
           uint32_t cv[3];  // RQT column of each variable member
@@ -889,6 +902,7 @@ __global__ void __launch_bounds__(GROUP_MAX_BD, GCfg<N>::PERM ? BOTE_GROUP_WAVES
               }
             }
           }
+          GASSERT(a, bi < (uint32_t)N, 7);  // leader member
           if (amb) {
             defer_rank(a, rank);
             have = false;
@@ -946,6 +960,11 @@ __global__ void __launch_bounds__(GROUP_MAX_BD, GCfg<N>::PERM ? BOTE_GROUP_WAVES
                 us2 lo, hi;
                 nearest(lines_c, g8, lo, hi);
                 const uint32_t L = as_u32(lo), H = as_u32(hi);
+#ifdef BOTE_DEBUG
+                // every client's nearest-member tag names a member (low 4 bits)
+                GASSERT(a, (L & 15u) < (uint32_t)N && ((L >> 16) & 15u) < (uint32_t)N && (H & 15u) < (uint32_t)N &&
+                               ((H >> 16) & 15u) < (uint32_t)N, 8);
+#endif
                 const us2 dlo = lo >> (us2)4, dhi = hi >> (us2)4;
                 auto acc1 = [&](int t, us2 q01, us2 q23) {
                   // packed adds as one 32-bit add: no carry crosses the halves
@@ -1252,10 +1271,17 @@ static hipError_t launch_group_n(const FastArgs& a, uint32_t grid, size_t shm, h
   return hipGetLastError();
 }
 
-static const void* group_fn(uint32_t n, bool def) {
+// The instantiation launch_group runs for these arguments (its occupancy
+// decides the persistent grid, so it must be the kernel that runs).
+static bool group_si(const FastArgs& a) { return a.srv_identity && a.want_digest && a.ft_metric == 2; }
+static const void* group_fn(const FastArgs& a, uint32_t n, bool def) {
   switch (n) {
-#define FN_CASE(NN) \
-  case NN: return def ? (const void*)sweep_group_kernel<NN, true, false, false> : (const void*)sweep_group_kernel<NN, false, false, false>;
+#define FN_CASE(NN)                                                                                       \
+  case NN:                                                                                                \
+    return def ? (group_si(a) ? (a.grx ? (const void*)sweep_group_kernel<NN, true, true, true>            \
+                                       : (const void*)sweep_group_kernel<NN, true, true, false>)          \
+                              : (const void*)sweep_group_kernel<NN, true, false, false>)                  \
+               : (const void*)sweep_group_kernel<NN, false, false, false>;
     FN_CASE(4) FN_CASE(5) FN_CASE(6) FN_CASE(7) FN_CASE(8) FN_CASE(9) FN_CASE(10) FN_CASE(11) FN_CASE(12)
     FN_CASE(13) FN_CASE(14) FN_CASE(15) FN_CASE(16)
 #undef FN_CASE
@@ -1263,12 +1289,12 @@ static const void* group_fn(uint32_t n, bool def) {
   }
 }
 
-int group_occupancy(uint32_t n, size_t shm, bool def, uint32_t bd) {
+int group_occupancy(const FastArgs& a, uint32_t n, size_t shm, bool def) {
   int nb = 0;
-  const void* k = group_fn(n, def);
+  const void* k = group_fn(a, n, def);
   if (!k) return 0;
   if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm) != hipSuccess) return 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, (int)bd, shm) != hipSuccess) return 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, (int)a.gbd, shm) != hipSuccess) return 0;
   return nb > 0 ? nb : 0;
 }
 
@@ -1276,7 +1302,7 @@ hipError_t launch_group(const FastArgs& a, uint32_t n, bool def, uint32_t grid, 
   switch (n) {
 #define GS_CASE(NN) \
   case NN:                                                                                           \
-    return def ? (a.srv_identity && a.want_digest && a.ft_metric == 2                               \
+    return def ? (group_si(a)                                                                        \
                       ? (a.grx ? launch_group_n<NN, true, true, true>(a, grid, shm, st)              \
                                : launch_group_n<NN, true, true, false>(a, grid, shm, st))             \
                       : launch_group_n<NN, true, false, false>(a, grid, shm, st))                    \

@@ -121,6 +121,13 @@ struct FastArgs {
   uint64_t* queue;  // deferred near-tie configs (colex ranks)
   unsigned long long* queue_count;
   uint64_t queue_cap;
+#ifdef BOTE_DEBUG
+  // Device-assert builds only (scripts/build_variant.sh debug -DBOTE_DEBUG):
+  // failed bounds checks set bits in *dbg_flag (soft asserts: no trap, the
+  // kernel keeps running) and bote_sweep_result reports BOTE_E_DEVICE.
+  unsigned int* dbg_flag;
+  uint64_t lowtab_n;  // entries of lowtab
+#endif
 #ifdef BOTE_ABLATION
   // Timing-diagnostics builds only (scripts/build_variant.sh NAME -DBOTE_ABLATION,
   // env BOTE_ABLATE; results are wrong when set).  The product library is
@@ -131,6 +138,17 @@ struct FastArgs {
   uint32_t ablate;
 #endif
 };
+#ifdef BOTE_DEBUG
+// bit `code` of *dbg_flag when `cond` fails (codes: DESIGN.md §5, debug build)
+#define GASSERT(a, cond, code)                                                    \
+  do {                                                                            \
+    if (!(cond)) atomicOr((a).dbg_flag, 1u << (code));                            \
+  } while (0)
+#else
+#define GASSERT(a, cond, code) \
+  do {                         \
+  } while (0)
+#endif
 #ifdef BOTE_ABLATION
 #define ABLATE(a, bit) (((a).ablate & (bit)) != 0)
 #else
@@ -141,7 +159,9 @@ int fast_occupancy(uint32_t n, size_t shm);
 hipError_t launch_fast(const FastArgs& a, uint32_t n, uint32_t grid, size_t shm, hipStream_t st);
 size_t group_smem_bytes(const FastArgs& a, uint32_t n);
 bool group_uses_lines(uint32_t n);  // n <= 7: client lines (FastArgs::gslots) and register lookups
-int group_occupancy(uint32_t n, size_t shm, bool def_objectives, uint32_t bd);
+// workgroups per CU of the kernel instantiation launch_group runs for `a`
+// (workgroup size a.gbd)
+int group_occupancy(const FastArgs& a, uint32_t n, size_t shm, bool def_objectives);
 hipError_t launch_group(const FastArgs& a, uint32_t n, bool def_objectives, uint32_t grid, size_t shm, hipStream_t st);
 
 size_t eval_smem_bytes(const EvalArgs& a, uint32_t n, uint32_t bd, bool topk);

@@ -10,6 +10,7 @@ this build's replacement.
 """
 from __future__ import annotations
 
+import os
 from typing import Tuple
 
 
@@ -69,8 +70,15 @@ def sharded_sweep(sweep, stream=None, group=None, device=None):
     sweep.result_device(blk.data_ptr(), stream)
     if world == 1:
         return sweep.parse_block(blk.cpu().numpy())
-    gathered = torch.empty(world * nbytes, dtype=torch.uint8, device=device)
-    dist.all_gather_into_tensor(gathered, blk, group=group)
+    if device.type == "cuda" and dist.get_backend(group) == "gloo":
+        # gloo moves host memory: gather through the host (a rehearsal of
+        # the N-rank path with several ranks on one GPU; RCCL gathers on the device)
+        g = torch.empty(world * nbytes, dtype=torch.uint8)
+        dist.all_gather_into_tensor(g, blk.cpu(), group=group)
+        gathered = g.to(device)
+    else:
+        gathered = torch.empty(world * nbytes, dtype=torch.uint8, device=device)
+        dist.all_gather_into_tensor(gathered, blk, group=group)
     return merge_gathered(sweep, gathered, world, stream, device)
 
 
@@ -93,3 +101,34 @@ def merge_gathered(sweep, gathered, world: int, stream=None, device=None):
         src, n = nxt, groups
     sweep.merge_device(src.data_ptr(), n, out.data_ptr(), stream)
     return sweep.parse_block(out.cpu().numpy())
+
+
+def world_census(device=None, group=None):
+    """Every rank's (rank, local rank, device ordinal, device identity hash),
+    all-gathered over the data-path backend: the evidence that the collective
+    spans the ranks (and distinct GPUs) the bench line reports."""
+    import hashlib
+
+    import torch
+    import torch.distributed as dist
+
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    rank = dist.get_rank(group) if dist.is_initialized() else 0
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+    ident = 0
+    if dev.type == "cuda":
+        props = torch.cuda.get_device_properties(dev)
+        uid = str(getattr(props, "uuid", "")) + str(getattr(props, "pci_bus_id", "")) + props.name
+        ident = int.from_bytes(hashlib.sha256(uid.encode()).digest()[:7], "little")
+    mine = torch.tensor([rank, local, dev.index or 0, ident], dtype=torch.int64)
+    if world == 1:
+        rows = [mine.tolist()]
+    else:
+        on = dev if (dev.type == "cuda" and dist.get_backend(group) != "gloo") else torch.device("cpu")
+        out = torch.empty(world * 4, dtype=torch.int64, device=on)
+        dist.all_gather_into_tensor(out, mine.to(on), group=group)
+        rows = out.view(world, 4).cpu().tolist()
+    return {"ranks": sorted(r[0] for r in rows), "local_ranks": [r[1] for r in rows],
+            "distinct_devices": len({(r[2], r[3]) for r in rows}),
+            "backend": dist.get_backend(group) if dist.is_initialized() else None}

@@ -80,6 +80,7 @@ extern "C" {
 
 typedef struct bote_planet bote_planet;
 typedef struct bote_sweep bote_sweep;
+typedef struct bote_search bote_search;
 
 typedef struct {
   uint32_t kind; /* BOTE_OBJ_* */
@@ -273,15 +274,36 @@ int bote_sweep_deferred(bote_sweep* s, void* hip_stream, uint64_t* out);
 int bote_sweep_grid(const bote_sweep* s, uint32_t* out_grid, uint32_t* out_block, uint32_t* out_lds_bytes);
 int bote_sweep_destroy(bote_sweep* s);
 
-/* ------------------------------------------ multi-device search (one call) --- */
+/* ------------------------------------------------ multi-device search --- */
 /* The exhaustive search over colex ranks [rank_begin, rank_end) sharded over
  * n_devices planets (planets[i] lives on the device that sweeps shard i; a
- * device may appear more than once).  Shards run concurrently, one HIP stream
- * each; their result blocks are peer-copied to planets[0]'s device and merged
- * there by (key, rank).  Outputs as bote_sweep_result; the result equals one
- * unsharded sweep.  Replaces the rayon fork-join of Search::compute_all_configs
- * (search.rs:199-232) for a single client set.  Every planet must hold the
- * same latency matrix. */
+ * device may appear more than once).  Replaces the rayon fork-join of
+ * Search::compute_all_configs (fantoch_bote/src/search.rs:199-232) for a
+ * single client set, so its output is Search's streamed equivalent.  Every
+ * planet must hold the same latency matrix.
+ *
+ * bote_search_create does all host work once: one sweep, stream and result
+ * buffer per shard, the shard bounds (equal estimated cost, as
+ * bote_sweep_split) and each shard's work-chunk table, from ONE host walk of
+ * the rank space shared by all shards; it returns with the handle idle.
+ * bote_search_launch is device work only and asynchronous: every shard's
+ * sweep on its own stream, a peer copy of its result block to planets[0]'s
+ * device, and a (key, rank) merge tree there.  It may be called repeatedly
+ * (each launch recomputes the whole range).  bote_search_result waits for the
+ * last launch and copies out as bote_sweep_result; the result equals one
+ * unsharded sweep.  Calls on one handle must not overlap. */
+int bote_search_create(const bote_planet* const* planets, uint32_t n_devices,
+                       const uint32_t* servers, uint32_t ns, const uint32_t* clients, uint32_t nc,
+                       uint32_t n, uint64_t rank_begin, uint64_t rank_end,
+                       const bote_objective* objs, uint32_t n_obj, uint32_t K,
+                       const bote_ranking_params* rp, int digest, bote_search** out);
+int bote_search_launch(bote_search* h);
+int bote_search_result(bote_search* h, bote_topk_record* out, uint32_t* out_count,
+                       uint64_t* out_valid, uint64_t* out_digest);
+/* The shard bounds chosen at creation: n_devices + 1 ascending ranks. */
+int bote_search_bounds(const bote_search* h, uint64_t* out_bounds);
+int bote_search_destroy(bote_search* h);
+/* One-shot form: create + launch + result + destroy. */
 int bote_search_topk(const bote_planet* const* planets, uint32_t n_devices,
                      const uint32_t* servers, uint32_t ns, const uint32_t* clients, uint32_t nc,
                      uint32_t n, uint64_t rank_begin, uint64_t rank_end,

@@ -21,6 +21,11 @@ for f in bote_kernels bote_sweep bote_group bote_quorums bote_chain bote_capi; d
   done
   if [ $stale = 1 ]; then $H -I fantoch_amd/csrc -c $src -o $D/obj/$f.o & fi
 done
+# host-only code (plain C++)
+if [ ! -f $D/obj/bote_host.o ] || [ fantoch_amd/csrc/bote_host.cpp -nt $D/obj/bote_host.o ] || [ fantoch_amd/csrc/bote_host.hpp -nt $D/obj/bote_host.o ]; then
+  g++ -O2 -std=c++17 -fPIC $FLAGS -c fantoch_amd/csrc/bote_host.cpp -o $D/obj/bote_host.o &
+fi
 wait
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $D/libbote_hip.so $D/obj/*.o
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -Wl,--no-undefined -o $D/libbote_hip.so $D/obj/*.o
 echo built $D/libbote_hip.so
+# Device-assert variant (soft asserts):  scripts/build_variant.sh debug -DBOTE_DEBUG

@@ -55,3 +55,21 @@ def test_no_device_is_an_error_not_a_fallback():
     h = C.c_void_p()
     rc = _lib.lib().bote_planet_create(np.zeros(4, np.uint16), 2, 0, C.byref(h))
     assert rc == -6  # BOTE_E_NODEV
+
+
+def test_out_of_range_latency_and_size_are_errors():
+    """The device paths hold latencies in 14 bits (BOTE_MAX_LATENCY = 16383;
+    the packed fast/group paths need <= 4095 and fall back to the exact
+    generic kernel above it).  A larger latency, where the reference takes
+    any u64, is refused with BOTE_E_RANGE when the planet is created, before
+    any device call, so no eval/sweep entry point ever sees one."""
+    import ctypes as C
+
+    import numpy as np
+    h = C.c_void_p()
+    lat = np.zeros(9, np.uint16)
+    lat[1] = 16384
+    assert _lib.lib().bote_planet_create(lat, 3, 0, C.byref(h)) == -4  # BOTE_E_RANGE
+    assert "16383" in _lib.lib().bote_last_error().decode()
+    assert _lib.lib().bote_planet_create(np.zeros(129 * 129, np.uint16), 129, 0, C.byref(h)) == -4
+    assert not h.value

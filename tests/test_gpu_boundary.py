@@ -11,7 +11,8 @@ import pytest
 
 import oracle as O
 from fantoch_amd import _lib
-from fantoch_amd.bote import DEFAULT_OBJECTIVES, DEFAULT_RANKING, Bote, DevicePlanet, Sweep, search_topk
+from fantoch_amd.bote import (DEFAULT_OBJECTIVES, DEFAULT_RANKING, Bote, DevicePlanet, MultiDeviceSearch, Sweep,
+                              search_topk)
 from fantoch_amd.planet import Planet
 
 pytestmark = pytest.mark.gpu
@@ -51,6 +52,67 @@ def test_search_topk_full_r64n7_vs_oracle_fixture():
     got = search_topk(dps, srv, srv, 7)
     assert (got.valid, got.digest) == (fx["valid"], fx["digest"])
     assert got.tops == [[tuple(r) for r in t] for t in fx["tops"]]
+
+
+def test_search_handle_repeated_launch_is_device_work_only():
+    """bote_search_create/launch/result over devices [0, 0, 0] and the full
+    R=64 n=7 rank space: the handle's shard bounds are bote_sweep_split's,
+    every launch equals the oracle's full sweep, and a repeated launch (no
+    host walk, no allocation) costs about one single-device sweep."""
+    import time
+
+    path = os.path.join(GOLDEN, "syn_r64n7_full.json")
+    if not os.path.exists(path):
+        pytest.skip("fixture not generated yet (scripts/oracle_fixtures.sh)")
+    fx = json.load(open(path))
+    want = (fx["valid"], fx["digest"], [[tuple(r) for r in t] for t in fx["tops"]])
+    p = Planet.synthetic(64)
+    dps = [DevicePlanet(p) for _ in range(3)]
+    srv = np.arange(64, dtype=np.uint32)
+    h = MultiDeviceSearch(dps, srv, srv, 7)
+    sw = Sweep(dps[0], srv, srv, 7, DEFAULT_OBJECTIVES, K=100, ranking=DEFAULT_RANKING, digest=True)
+    assert h.bounds() == sw.split(0, sw.total, 3)
+    h.launch()
+    r = h.result()
+    assert (r.valid, r.digest, r.tops) == want
+    sw.launch()
+    sw.result()
+
+    def timed(fn, reps=5):
+        best = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            fn()
+            best.append(time.perf_counter() - t0)
+        return sorted(best)[reps // 2]
+
+    t_handle = timed(lambda: (h.launch(), h.result()))
+    t_single = timed(lambda: (sw.launch(), sw.result()))
+    print(f"search handle, 3 shards on one GPU: {t_handle * 1e3:.2f} ms per launch+result; "
+          f"single sweep {t_single * 1e3:.2f} ms; ratio {t_handle / t_single:.3f}")
+    r = h.result()
+    assert (r.valid, r.digest, r.tops) == want
+    assert t_handle < 1.25 * t_single
+
+
+def test_search_handle_errors_leave_no_state():
+    """Refused creations (planets that differ, a bad K, a bad range) return
+    their codes; handles created afterwards work."""
+    p = Planet.synthetic(64)
+    q = Planet.synthetic(64, seed=1)
+    srv = np.arange(64, dtype=np.uint32)
+    a, b = DevicePlanet(p), DevicePlanet(q)
+    with pytest.raises(_lib.BoteError, match="differ"):
+        MultiDeviceSearch([a, b], srv, srv, 7)
+    with pytest.raises(_lib.BoteError, match="K must be"):
+        MultiDeviceSearch([a, a], srv, srv, 7, K=0)
+    with pytest.raises(_lib.BoteError, match="out of bounds"):
+        MultiDeviceSearch([a], srv, srv, 7, rank_begin=10, rank_end=5)
+    h = MultiDeviceSearch([a, a], srv, srv, 7, rank_begin=1000, rank_end=200_000)
+    h.launch()
+    sw = Sweep(a, srv, srv, 7, DEFAULT_OBJECTIVES, K=100, ranking=DEFAULT_RANKING, digest=True)
+    sw.launch(1000, 200_000)
+    assert _same(h.result(), sw.result())
 
 
 def test_overflow_fallback_is_device_side():

@@ -489,6 +489,16 @@ def test_checkpointed_sweep_resumes(gcp, tmp_path):
     other = Sweep(dp, srv, srv, 5, DEFAULT_OBJECTIVES, K=100, ranking=DEFAULT_RANKING, digest=True)
     with pytest.raises(ValueError):
         other.run_checkpointed(ck)
+    # same n, K, lists and objectives, but scored under other RankingParams:
+    # its validity and score objective differ, so the checkpoint is refused
+    rk = RankingParams.new(100, 35, 0, 15, 3, 13, FTMetric.F1F2)
+    scored_other = Sweep(dp, srv, srv, 7, DEFAULT_OBJECTIVES, K=100, ranking=rk, digest=True)
+    with pytest.raises(ValueError):
+        scored_other.run_checkpointed(ck)
+    # and without the digest
+    nodig = Sweep(dp, srv, srv, 7, DEFAULT_OBJECTIVES, K=100, ranking=DEFAULT_RANKING, digest=False)
+    with pytest.raises(ValueError):
+        nodig.run_checkpointed(ck)
 
 
 def test_search_r17cmaxn_client_sets(gcp):
