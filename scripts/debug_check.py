@@ -20,7 +20,8 @@ def main():
 
     assert "lib_debug" in _lib.LIB_PATH, "run with BOTE_LIB_PATH pointing at the debug build"
     gold = os.path.join(ROOT, "tests", "golden")
-    cases = json.load(open(os.path.join(gold, "topk.json")))["cases"]
+    t = json.load(open(os.path.join(gold, "topk.json")))
+    cases, K = t["cases"], t["K"]
     gcp = Planet.new()
     dp = DevicePlanet(gcp, 0)
     planets = {None: (gcp, dp)}
@@ -32,14 +33,13 @@ def main():
             planets[R] = (p, DevicePlanet(p, 0))
         p, d = planets[R]
         srv = np.arange(p.R, dtype=np.uint32)
-        sw = Sweep(d, srv, srv, fx["n"], DEFAULT_OBJECTIVES, K=fx.get("K", 100), ranking=DEFAULT_RANKING,
+        sw = Sweep(d, srv, srv, fx["n"], DEFAULT_OBJECTIVES, K=K, ranking=DEFAULT_RANKING,
                    digest=True, kernel="group")
         sw.launch(fx["rank_begin"], fx["rank_end"])
         r = sw.result()  # raises on a device assert
-        K = len(r.tops[0]) if r.tops else 0
-        ok = (r.valid, r.digest) == (int(fx["valid"]), int(fx["digest"])) and all(
-            [tuple(map(int, x)) for x in t] == [(int(k), int(rk)) for k, rk in ft[:len(t)]]
-            for t, ft in zip(r.tops, fx["tops"]))
+        ok = (r.valid, r.digest) == (int(fx["valid"]), int(fx["digest"])) and \
+            [[(int(k), int(rk)) for k, rk in lst] for lst in r.tops] == \
+            [[(int(k), int(rk)) for k, rk in lst] for lst in fx["tops"]]
         print(f"{name}: group kernel under BOTE_DEBUG, {fx['rank_end'] - fx['rank_begin']} configs, "
               f"asserts clean, result {'equals' if ok else 'DIFFERS FROM'} the oracle fixture (K={K})", flush=True)
         if not ok:
