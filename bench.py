@@ -60,12 +60,30 @@ def work_per_config_group(n: int, C: int) -> int:
     return 3 * (n - 1) + 3 * (n - 3) + 4 * C + n + (1 + mf) * (C + n) + 3 * n + 4 * mf + n + 2 * (1 + mf) * (C + n)
 
 
+def work_per_config_keys(n: int, C: int) -> int:
+    """W' of the extended key set (BASELINE config 5, DESIGN.md §5): W' plus,
+    per Tempo quorum table the compute_stats keys lack (NX: 2 at n = 6, 7 --
+    q = 2, 3), one add, one sum and one square per client (Input + colocated),
+    and per leader and f the FPaxos moments from the column sums (3 ops) and
+    the best-by-mean compare (1 op).  R=128 n=6: 1,780 + 804 + 48 = 2,632."""
+    mf = min(n // 2, 2)
+    m = n // 2
+    base = {m + f for f in range(1, mf + 1)} | {m + (m + 1) // 2}
+    ext = {2} | ({3, 4} if mf >= 2 else set())
+    nx = len(ext - base)
+    return work_per_config_group(n, C) + 3 * nx * (C + n) + 4 * mf * n
+
+
 def workloads():
     return {
-        "r64n7": dict(R=64, n=7, desc="synthetic R=64 planet (splitmix64 seed 0x5EED0064), n=7, f=1,2, "
-                                     "clients = all 64 regions + colocated"),
-        "r128n6": dict(R=128, n=6, desc="synthetic R=128 planet (seed 0x5EED0128), n=6, f=1,2"),
-        "gcp": dict(R=None, n=5, desc="GCP 20-region planet, n=5"),
+        "r64n7": dict(R=64, n=7, keys=0, desc="synthetic R=64 planet (splitmix64 seed 0x5EED0064), n=7, f=1,2, "
+                                              "clients = all 64 regions + colocated"),
+        "r128n6": dict(R=128, n=6, keys=1, desc="BASELINE config 5: synthetic R=128 planet (seed 0x5EED0128), n=6, "
+                                                "f=1,2, compute_stats keys + Tempo tiny/write keys + FPaxos all "
+                                                "leaders (BOTE_KEYS_TEMPO_ALL_LEADERS), 8 objectives"),
+        "r128n6_base": dict(R=128, n=6, keys=0, desc="synthetic R=128 planet (seed 0x5EED0128), n=6, f=1,2, "
+                                                     "the 10 compute_stats keys only"),
+        "gcp": dict(R=None, n=None, keys=0, desc="GCP 20-region planet, every config of n=3..13 step 2 (main_gcp)"),
     }
 
 
@@ -117,6 +135,112 @@ def cpu_baseline(planet, n, budget_s=10.0):
             "seconds": round(dn, 3), "nproc": os.cpu_count(), "cpu_share": share,
             "single_thread": {"value": c1 / d1, "unit": "configs/s", "cores": 1, "sample": f"{c1} ranks from {mid}",
                               "seconds": round(d1, 3)}}
+
+
+GCP_NS = (3, 5, 7, 9, 11, 13)  # Search::compute_configs: n in (min_n..=max_n).step_by(2) (search.rs:241-246)
+
+
+def cpu_baseline_gcp(planet, ns=GCP_NS):
+    """SURVEY.md §8d for BASELINE configs 1 and 2: the reference-faithful CPU
+    restatement (oracle/, 'port') over EVERY GCP config, in full: config 1
+    (n = 3, 5) and config 2 (n = 3..13 step 2, the reference's own
+    compute_configs), at 1 thread (the reference's parallelism for one client
+    set, search.rs:209-211) and at this job's CPU share."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import numpy as np
+
+    import oracle as O
+    from fantoch_amd import _lib
+    from fantoch_amd.bote import DEFAULT_OBJECTIVES
+
+    o = O.OraclePlanet.of(planet)
+    srv = np.arange(planet.R, dtype=np.uint32)
+    share = host_cpu_share()
+
+    def run(nset, threads):
+        cfgs, t0 = 0, time.perf_counter()
+        for n in nset:
+            total = _lib.binomial(planet.R, n)
+            o.sweep(srv, srv, n, 0, total, DEFAULT_OBJECTIVES, 100, (110.0, 35.0, 0.0, 15.0), 2, threads)
+            cfgs += total
+        dt = time.perf_counter() - t0
+        return {"configs": cfgs, "seconds": round(dt, 3), "value": cfgs / dt, "threads": threads}
+
+    c2_1, c2_n = run(ns, 1), run(ns, share)
+    c1_1, c1_n = run((3, 5), 1), run((3, 5), share)
+    return {"value": c2_n["value"], "unit": "configs/s", "cores": share, "kind": "port",
+            "sample": f"every GCP config of n = {list(ns)} ({c2_n['configs']} configs), in full: compute_stats + "
+                      f"compute_score + top-K per config (oracle/bote_oracle.cpp, std::thread x {share})",
+            "nproc": os.cpu_count(), "cpu_share": share,
+            "config2_single_thread": c2_1, "config2_all": c2_n, "config1_single_thread": c1_1, "config1_all": c1_n}
+
+
+def main_gcp(args):
+    """BASELINE configs 1-2 on one GPU: a step sweeps EVERY GCP config of
+    n = 3..13 step 2 (507,604 configs; the reference's compute_configs) with
+    compute_stats + compute_score + the device top-K, each n checked against
+    its oracle fixture (tests/golden/topk.json).  Launch-bound: these are
+    parity cases next to the CPU baseline, not the headline."""
+    import numpy as np
+    import torch
+
+    from fantoch_amd import _lib
+    from fantoch_amd.bote import DEFAULT_OBJECTIVES, DEFAULT_RANKING, DevicePlanet, Sweep
+    from fantoch_amd.planet import Planet
+
+    if int(os.environ.get("WORLD_SIZE", "1")) != 1 or args.gpus != 1:
+        sys.exit("bench.py: --workload gcp runs on one GPU")
+    torch.cuda.set_device(0)
+    planet = Planet.new()
+    dp = DevicePlanet(planet, 0)
+    srv = np.arange(planet.R, dtype=np.uint32)
+    sweeps = [Sweep(dp, srv, srv, n, DEFAULT_OBJECTIVES, K=100, ranking=DEFAULT_RANKING, digest=True) for n in GCP_NS]
+    stream = torch.cuda.current_stream().cuda_stream
+    total = sum(sw.total for sw in sweeps)
+
+    def step():
+        for sw in sweeps:
+            sw.launch(0, sw.total, stream)
+        return [sw.result(stream) for sw in sweeps]
+
+    for _ in range(args.warmup):
+        res = step()
+    torch.cuda.synchronize()
+    for sw in sweeps:
+        sw.timing_reset()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        res = step()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    kern = sum(sw.timing()[0] for sw in sweeps) / max(args.steps, 1)
+    fx = json.load(open(os.path.join(ROOT, "tests", "golden", "topk.json")))
+    for n, r in zip(GCP_NS, res):
+        c = fx["cases"][f"gcp_n{n}"]
+        K = fx["K"]
+        if (r.valid, str(r.digest)) != (c["valid"], c["digest"]) or \
+                [[[str(k), rk] for k, rk in lst[:K]] for lst in r.tops] != c["tops"]:
+            sys.exit(f"bench.py: GCP n={n} differs from the oracle fixture tests/golden/topk.json")
+    W = sum(sw.total * work_per_config(sw.n, planet.R) for sw in sweeps)
+    achieved = W / (kern * 1e-3) / 1e12
+    out = {
+        "metric": "region configs evaluated/sec, GCP 20-region planet, every config of n=3..13 step 2 (BASELINE "
+                  "configs 1-2: the reference's compute_configs)",
+        "value": total * args.steps / dt, "unit": "configs/s", "n_gpus": 1, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3, "higher_is_better": True, "scaling": "strong",
+        "vs_baseline": None, "dtype": "u32", "data": "gcp",
+        "config": {"workload": "GCP R=20 (latency_gcp), n = 3,5,7,9,11,13, all configs, 10 keys, 5 objectives, K=100",
+                   "configs_per_step": total, "kernel_paths": [sw.kernel_path() for sw in sweeps]},
+        "roofline": {"bound": "launch", "achieved": achieved, "peak": VALU_PEAK_TOPS, "unit": "Tops/s",
+                     "frac": achieved / VALU_PEAK_TOPS, "traffic": None, "work_per_config": "SURVEY W(n, 20)",
+                     "kernel_ms_per_step": kern,
+                     "note": "six sweeps of 1,140..167,960 configs: launch- and merge-bound, not a roofline case"},
+        "result_check": {"fixture": "every n equal to tests/golden/topk.json (oracle, all ranks)",
+                         "valid": [r.valid for r in res]},
+    }
+    if not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline_gcp(planet)
+    print(json.dumps(out), flush=True)
 
 
 def load_fixture(workload):
@@ -177,6 +301,9 @@ def main():
 
         sys.exit(run_world(args.gpus, [os.path.abspath(__file__)] + sys.argv[1:]))
 
+    if args.workload == "gcp":
+        return main_gcp(args)
+
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -198,7 +325,7 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", dev_index))
 
     from fantoch_amd import _lib
-    from fantoch_amd.bote import DEFAULT_OBJECTIVES, DEFAULT_RANKING, DevicePlanet, Sweep
+    from fantoch_amd.bote import CONFIG5_OBJECTIVES, DEFAULT_OBJECTIVES, DEFAULT_RANKING, DevicePlanet, Sweep
     from fantoch_amd.dist import shard_of, sharded_sweep, world_census
     from fantoch_amd.planet import Planet
 
@@ -209,7 +336,8 @@ def main():
     srv = np.arange(planet.R, dtype=np.uint32)
     # digest=True: every config's 10 histogram moments and leader feed a
     # checksum, so none of compute_stats' work can be skipped.
-    sweep = Sweep(dp, srv, srv, n, DEFAULT_OBJECTIVES, K=100, ranking=DEFAULT_RANKING, digest=True)
+    objectives = CONFIG5_OBJECTIVES if wl["keys"] else DEFAULT_OBJECTIVES
+    sweep = Sweep(dp, srv, srv, n, objectives, K=100, ranking=DEFAULT_RANKING, digest=True, keys=wl["keys"])
     total = sweep.total
     b, e = shard_of(sweep, world, rank)  # equal estimated cost (bote_sweep_split)
     stream = torch.cuda.current_stream().cuda_stream
@@ -257,7 +385,7 @@ def main():
 
     if rank == 0:
         W = work_per_config(n, planet.R)
-        Wg = work_per_config_group(n, planet.R)
+        Wg = work_per_config_keys(n, planet.R) if wl["keys"] else work_per_config_group(n, planet.R)
         shard = e - b
         achieved = shard * Wg / (kavg_ms * 1e-3) / 1e12  # T int-ops/s of W', dominant kernel
         traffic = load_traffic(f"{args.workload}_n{world}")
@@ -285,12 +413,14 @@ def main():
             "dtype": "u32",
             "data": "synthetic" if wl["R"] else "gcp",
             "config": {"workload": wl["desc"], "regions": planet.R, "n": n, "configs_per_step": total,
-                       "keys": 10, "objectives": len(DEFAULT_OBJECTIVES), "K": 100,
+                       "keys": 20 if wl["keys"] else 10, "key_set": wl["keys"], "objectives": len(objectives),
+                       "K": 100,
                        "parallelism": f"rank-shard x{world}", "grid": grid, "block": block, "lds_bytes": lds,
                        "kernel_path": sweep.kernel_path()},
             "roofline": {"bound": "valu", "achieved": achieved, "peak": VALU_PEAK_TOPS, "unit": "Tops/s",
                          "frac": achieved / VALU_PEAK_TOPS, "traffic": traffic,
-                         "work_per_config": Wg, "work_def": "W' (DESIGN.md §5, bench.work_per_config_group)",
+                         "work_per_config": Wg,
+                         "work_def": "W' (DESIGN.md §5, bench.work_per_config_%s)" % ("keys" if wl["keys"] else "group"),
                          "survey_w": W, "survey_w_frac": shard * W / (kavg_ms * 1e-3) / 1e12 / VALU_PEAK_TOPS,
                          "valu_issue": valu, "kernel_ms_avg": kavg_ms,
                          "kernel": KERNEL_NAMES[sweep.kernel_path()]},

@@ -26,6 +26,12 @@ FPAXOS, EPAXOS, ATLAS, TEMPO, TEMPO_TINY = 0, 1, 2, 3, 4
 STAT_MEAN, STAT_COV, STAT_MDTM = 0, 1, 2
 SLOT_AF1, SLOT_FF1, SLOT_AF2, SLOT_FF2, SLOT_E = 0, 1, 2, 3, 4
 SLOT_NAMES = ["af1", "ff1", "af2", "ff2", "e", "af1C", "ff1C", "af2C", "ff2C", "eC"]
+# the extended key set (BOTE_KEYS_TEMPO_ALL_LEADERS, include/bote_hip.h)
+KEYS_BASE, KEYS_TEMPO_ALL_LEADERS = 0, 1
+SLOT_TT1, SLOT_TT2, SLOT_TW1, SLOT_TW2, SLOT_FL1, SLOT_FL2 = 10, 11, 12, 13, 18, 19
+SLOT_X_COLOCATED = 4
+NSLOTS_X = 20
+SLOT_NAMES_X = SLOT_NAMES + ["ttf1", "ttf2", "twf1", "twf2", "ttf1C", "ttf2C", "twf1C", "twf2C", "fl1", "fl2"]
 OBJ_SCORE, OBJ_MEAN, OBJ_COV = 0, 1, 2
 FT_F1, FT_F1F2 = 1, 2
 KP = 128
@@ -40,6 +46,7 @@ EXPORTS = [
     "bote_sweep_destroy", "bote_colex_unrank", "bote_binomial", "bote_sweep_timing_reset",
     "bote_sweep_timing", "bote_sweep_grid", "bote_sweep_is_fast", "bote_sweep_split", "bote_sweep_create_ex", "bote_search_topk", "bote_sweep_deferred", "bote_eval_leaderless", "bote_evolving_chains",
     "bote_search_create", "bote_search_launch", "bote_search_result", "bote_search_bounds", "bote_search_destroy",
+    "bote_eval_keys", "bote_sweep_create_keys",
 ]
 KERNELS = {None: 0, "auto": 0, "generic": 1, "fast": 2, "group": 3}
 
@@ -120,13 +127,18 @@ def lib():
     L.bote_sweep_create_ex.argtypes = [_vp, _u32p, C.c_uint32, _u32p, C.c_uint32, C.c_uint32,
                                        C.POINTER(Objective), C.c_uint32, C.c_uint32,
                                        C.POINTER(RankingParamsC), C.c_int, C.c_int, C.POINTER(_vp)]
+    L.bote_eval_keys.argtypes = [_vp, _u32p, C.c_uint32, _u32p, C.c_uint32, C.c_uint32, _vp, C.c_uint64, C.c_uint64,
+                                 C.c_uint32, _vp, _vp, _vp, _vp, _vp]
+    L.bote_sweep_create_keys.argtypes = [_vp, _u32p, C.c_uint32, _u32p, C.c_uint32, C.c_uint32,
+                                         C.POINTER(Objective), C.c_uint32, C.c_uint32,
+                                         C.POINTER(RankingParamsC), C.c_int, C.c_int, C.c_uint32, C.POINTER(_vp)]
     L.bote_search_topk.argtypes = [C.POINTER(_vp), C.c_uint32, _u32p, C.c_uint32, _u32p, C.c_uint32, C.c_uint32,
                                    C.c_uint64, C.c_uint64, C.POINTER(Objective), C.c_uint32, C.c_uint32,
                                    C.POINTER(RankingParamsC), C.c_int, C.POINTER(TopKRecord), _vp,
                                    C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
     L.bote_search_create.argtypes = [C.POINTER(_vp), C.c_uint32, _u32p, C.c_uint32, _u32p, C.c_uint32, C.c_uint32,
                                      C.c_uint64, C.c_uint64, C.POINTER(Objective), C.c_uint32, C.c_uint32,
-                                     C.POINTER(RankingParamsC), C.c_int, C.POINTER(_vp)]
+                                     C.POINTER(RankingParamsC), C.c_int, C.c_uint32, C.POINTER(_vp)]
     L.bote_search_launch.argtypes = [_vp]
     L.bote_search_result.argtypes = [_vp, C.POINTER(TopKRecord), _vp, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
     L.bote_search_bounds.argtypes = [_vp, C.POINTER(C.c_uint64)]

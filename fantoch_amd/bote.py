@@ -176,6 +176,43 @@ def eval_leaderless(dp: DevicePlanet, servers: Sequence[int], clients: Sequence[
     return LeaderlessResult(n, nc, [int(q) for q in qs], vals, s1, s2)
 
 
+@dataclass
+class KeysResult:
+    """bote_eval_keys outputs: exact moments of the extended key set."""
+    n: int
+    s1: np.ndarray       # (ncfg, 20) uint64; ~0 where a slot is absent
+    s2: np.ndarray       # (ncfg, 20) uint64
+    al_s1: np.ndarray    # (ncfg, 2, n) uint64: every leader's FPaxos sum, f = 1, 2, config order
+    al_s2: np.ndarray
+    leader: np.ndarray   # (ncfg,) the COV-best FPaxos leader (compute_stats)
+
+
+def eval_keys(dp: DevicePlanet, servers: Sequence[int], clients: Sequence[int], n: int,
+              configs: Optional[np.ndarray] = None, rank_begin: int = 0, ncfg: Optional[int] = None,
+              keys: int = _lib.KEYS_TEMPO_ALL_LEADERS) -> KeysResult:
+    """The extended key set per config (BASELINE config 5: Tempo tiny/write
+    keys, config.rs:317-329, and FPaxos all leaders, lib.rs:129-150) as exact
+    moments, from the device (bote_eval_keys)."""
+    srv, cli = u32(servers), u32(clients)
+    if configs is not None:
+        cfg = np.ascontiguousarray(np.asarray(configs, dtype=np.uint32).reshape(-1, n))
+        ncfg = cfg.shape[0]
+        cptr = ptr(cfg)
+    else:
+        cfg, cptr = None, None
+        if ncfg is None:
+            ncfg = _lib.binomial(len(srv), n) - rank_begin
+    ns_ = _lib.NSLOTS_X if keys else 10
+    s1 = np.zeros((ncfg, ns_), np.uint64)
+    s2 = np.zeros((ncfg, ns_), np.uint64)
+    a1 = np.zeros((ncfg, 2, n), np.uint64)
+    a2 = np.zeros((ncfg, 2, n), np.uint64)
+    lead = np.zeros(ncfg, np.uint32)
+    check(lib().bote_eval_keys(dp.h, srv, len(srv), cli, len(cli), n, cptr, rank_begin, ncfg, keys, ptr(lead),
+                               ptr(s1), ptr(s2), ptr(a1) if keys else None, ptr(a2) if keys else None))
+    return KeysResult(n, s1, s2, a1, a2, lead)
+
+
 def tempo_quorums(n: int) -> List[Tuple[Protocol, int, int]]:
     """(protocol, f, quorum size) of Tempo's fast (non-tiny, tiny) and write
     quorums for f = 1..max_f(n) (config.rs:317-329; max_f: search.rs:474-477)."""
@@ -654,6 +691,11 @@ def compute_score_host(n: int, stats: ProtocolStats, p: RankingParams) -> Tuple[
 DEFAULT_OBJECTIVES = [(_lib.OBJ_SCORE, 0), (_lib.OBJ_MEAN, _lib.SLOT_AF1), (_lib.OBJ_MEAN, _lib.SLOT_FF1),
                       (_lib.OBJ_COV, _lib.SLOT_AF1), (_lib.OBJ_MEAN, _lib.SLOT_E)]
 DEFAULT_RANKING = RankingParams.new(110, 35, 0, 15, 3, 13, FTMetric.F1F2)
+# BASELINE config 5 (the extended key set): the default objectives, then the
+# best Tempo tiny (f = 1) and write (f = 2) means and the best mean under
+# FPaxos's mean-optimal leader (all leaders), Input
+CONFIG5_OBJECTIVES = DEFAULT_OBJECTIVES + [(_lib.OBJ_MEAN, _lib.SLOT_TT1), (_lib.OBJ_MEAN, _lib.SLOT_TW2),
+                                           (_lib.OBJ_MEAN, _lib.SLOT_FL1)]
 
 
 @dataclass
@@ -668,19 +710,20 @@ class Sweep:
 
     def __init__(self, dp: DevicePlanet, servers: Sequence[int], clients: Sequence[int], n: int,
                  objectives=DEFAULT_OBJECTIVES, K: int = 100, ranking: Optional[RankingParams] = DEFAULT_RANKING,
-                 digest: bool = False, kernel: Optional[str] = None):
+                 digest: bool = False, kernel: Optional[str] = None, keys: int = _lib.KEYS_BASE):
         """kernel: None/'auto' (the library's choice), or force 'generic', 'fast'
-        or 'group' (every path is exact; bote_sweep_create_ex)."""
-        self.dp, self.n, self.K = dp, n, K
+        or 'group' (every path is exact; bote_sweep_create_keys).  keys: the
+        key set (_lib.KEYS_BASE, or KEYS_TEMPO_ALL_LEADERS for BASELINE config 5)."""
+        self.dp, self.n, self.K, self.keys = dp, n, K, keys
         self.servers, self.clients = u32(servers), u32(clients)
         self.objectives = list(objectives)
         self.ranking, self.digest = ranking, bool(digest)
         objs = (_lib.Objective * max(len(self.objectives), 1))(*[_lib.Objective(k, s) for k, s in self.objectives])
         rp = C.byref(_lib.ranking_params_c(ranking)) if ranking is not None else None
         h = C.c_void_p()
-        check(lib().bote_sweep_create_ex(dp.h, self.servers, len(self.servers), self.clients, len(self.clients), n,
-                                         objs, len(self.objectives), K, rp, 1 if digest else 0,
-                                         _lib.KERNELS[kernel], C.byref(h)))
+        check(lib().bote_sweep_create_keys(dp.h, self.servers, len(self.servers), self.clients, len(self.clients), n,
+                                           objs, len(self.objectives), K, rp, 1 if digest else 0,
+                                           _lib.KERNELS[kernel], keys, C.byref(h)))
         self.h = h
         self.total = _lib.binomial(len(self.servers), n)
 
@@ -713,7 +756,7 @@ class Sweep:
                            rk.min_mean_decrease], np.float64).view(np.uint64).tolist() + [rk.ft_metric.value]
                  if rk is not None else [0xFFFFFFFFFFFFFFFF] * 5)
         ident = np.concatenate([np.array([self.n, self.K, rank_begin, re, len(self.servers), len(self.clients),
-                                          int(self.digest)] + rbits, np.uint64),
+                                          int(self.digest), int(self.keys)] + rbits, np.uint64),
                                 self.servers.astype(np.uint64), self.clients.astype(np.uint64),
                                 np.asarray(self.objectives, np.uint64).reshape(-1),
                                 np.asarray(self.dp.planet.lat, np.uint64).reshape(-1)])
@@ -847,7 +890,8 @@ class MultiDeviceSearch:
 
     def __init__(self, planets: Sequence[DevicePlanet], servers: Sequence[int], clients: Sequence[int], n: int,
                  objectives=DEFAULT_OBJECTIVES, K: int = 100, ranking: Optional[RankingParams] = DEFAULT_RANKING,
-                 digest: bool = True, rank_begin: int = 0, rank_end: Optional[int] = None):
+                 digest: bool = True, rank_begin: int = 0, rank_end: Optional[int] = None,
+                 keys: int = _lib.KEYS_BASE):
         srv, cli = u32(servers), u32(clients)
         self.objectives, self.K, self.n_shards = list(objectives), K, len(planets)
         no = len(self.objectives)
@@ -859,7 +903,7 @@ class MultiDeviceSearch:
         self.rank_end = _lib.binomial(len(srv), n) if rank_end is None else rank_end
         h = C.c_void_p()
         check(lib().bote_search_create(hs, len(planets), srv, len(srv), cli, len(cli), n, rank_begin, self.rank_end,
-                                       objs, no, K, rp, 1 if digest else 0, C.byref(h)))
+                                       objs, no, K, rp, 1 if digest else 0, keys, C.byref(h)))
         self.h = h
 
     def __del__(self):

@@ -116,7 +116,7 @@ struct bote_planet {
   uint32_t* d_mat = nullptr;
   hipStream_t stream = nullptr;
   mutable std::mutex mu;
-  mutable DBuf ws[12];
+  mutable DBuf ws[14];
 };
 
 struct bote_sweep {
@@ -380,11 +380,13 @@ static void fill_rank_params(EvalArgs& a, const bote_ranking_params* rp) {
 }
 
 // ------------------------------------------------------------------- eval
-int bote_eval(const bote_planet* p, const uint32_t* servers, uint32_t ns, const uint32_t* clients, uint32_t nc,
-              uint32_t n, const uint32_t* configs, uint64_t rank_begin, uint64_t ncfg, const bote_ranking_params* rp,
-              uint32_t* out_vals, uint32_t* out_leader, uint64_t* out_sum, uint64_t* out_sumsq, double* out_mean,
-              double* out_cov, double* out_score, uint8_t* out_valid) {
+static int eval_impl(const bote_planet* p, const uint32_t* servers, uint32_t ns, const uint32_t* clients,
+                     uint32_t nc, uint32_t n, const uint32_t* configs, uint64_t rank_begin, uint64_t ncfg,
+                     const bote_ranking_params* rp, uint32_t keys, uint32_t* out_vals, uint32_t* out_leader,
+                     uint64_t* out_sum, uint64_t* out_sumsq, double* out_mean, double* out_cov, double* out_score,
+                     uint8_t* out_valid, uint64_t* out_al_sum, uint64_t* out_al_sumsq) {
   int rc;
+  if (keys > BOTE_KEYS_TEMPO_ALL_LEADERS) return fail(BOTE_E_ARG, "unknown key set");
   if ((rc = check_search_args(p, servers, ns, clients, nc, n))) return rc;
   if (rp && rp->ft_metric != BOTE_FT_F1 && rp->ft_metric != BOTE_FT_F1F2) return fail(BOTE_E_ARG, "bad ft_metric");
   if (ncfg == 0) return BOTE_OK;
@@ -406,9 +408,10 @@ int bote_eval(const bote_planet* p, const uint32_t* servers, uint32_t ns, const 
   HIP_TRY(hipSetDevice(p->device));
   hipStream_t st = p->stream;
   const size_t stride = 5ull * nc + 5ull * n;
+  const size_t NS = keys ? BOTE_NSLOTS_X : bote::NSLOT;
   DBuf &ds = p->ws[0], &dc = p->ws[1], &dcfg = p->ws[2], &dbin = p->ws[3], &dvals = p->ws[4], &dlead = p->ws[5],
        &ds1 = p->ws[6], &ds2 = p->ws[7], &dmean = p->ws[8], &dcov = p->ws[9], &dscore = p->ws[10],
-       &dvalid = p->ws[11];
+       &dvalid = p->ws[11], &dal1 = p->ws[12], &dal2 = p->ws[13];
   HIP_TRY(ds.reserve(ns * 4));
   HIP_TRY(dc.reserve(nc * 4));
   HIP_TRY(hipMemcpyAsync(ds.p, servers, ns * 4, hipMemcpyHostToDevice, st));
@@ -437,34 +440,56 @@ int bote_eval(const bote_planet* p, const uint32_t* servers, uint32_t ns, const 
     a.re = rank_begin + ncfg;
   }
   a.runlen = 1;
+  a.keys = keys;
   fill_rank_params(a, rp);
   if (out_vals) { HIP_TRY(dvals.reserve(ncfg * stride * 4)); a.out_vals = dvals.as<uint32_t>(); }
   if (out_leader) { HIP_TRY(dlead.reserve(ncfg * 4)); a.out_leader = dlead.as<uint32_t>(); }
-  if (out_sum) { HIP_TRY(ds1.reserve(ncfg * bote::NSLOT * 8)); a.out_s1 = ds1.as<uint64_t>(); }
-  if (out_sumsq) { HIP_TRY(ds2.reserve(ncfg * bote::NSLOT * 8)); a.out_s2 = ds2.as<uint64_t>(); }
-  if (out_mean) { HIP_TRY(dmean.reserve(ncfg * bote::NSLOT * 8)); a.out_mean = dmean.as<double>(); }
-  if (out_cov) { HIP_TRY(dcov.reserve(ncfg * bote::NSLOT * 8)); a.out_cov = dcov.as<double>(); }
+  if (out_sum) { HIP_TRY(ds1.reserve(ncfg * NS * 8)); a.out_s1 = ds1.as<uint64_t>(); }
+  if (out_sumsq) { HIP_TRY(ds2.reserve(ncfg * NS * 8)); a.out_s2 = ds2.as<uint64_t>(); }
+  if (out_mean) { HIP_TRY(dmean.reserve(ncfg * NS * 8)); a.out_mean = dmean.as<double>(); }
+  if (out_cov) { HIP_TRY(dcov.reserve(ncfg * NS * 8)); a.out_cov = dcov.as<double>(); }
+  const size_t nal = (size_t)ncfg * 2 * n;
+  if (keys && out_al_sum) { HIP_TRY(dal1.reserve(nal * 8)); a.out_al_s1 = dal1.as<uint64_t>(); }
+  if (keys && out_al_sumsq) { HIP_TRY(dal2.reserve(nal * 8)); a.out_al_s2 = dal2.as<uint64_t>(); }
   if (out_score && rp) { HIP_TRY(dscore.reserve(ncfg * 8)); a.out_score = dscore.as<double>(); }
   if (out_valid && rp) { HIP_TRY(dvalid.reserve(ncfg)); a.out_valid = dvalid.as<uint8_t>(); }
 
   const uint32_t bd = 256;
   size_t shm = bote::eval_smem_bytes(a, n, bd, false);
   if (shm > device_max_lds(p->device)) return fail(BOTE_E_RANGE, "planet/client set too large for LDS");
-  int nb = bote::eval_occupancy(n, true, bd, shm);
+  int nb = bote::eval_occupancy(n, true, bd, shm, keys != 0);
   uint64_t want = (ncfg + bd - 1) / bd;
   uint32_t grid = (uint32_t)std::min<uint64_t>(want, (uint64_t)device_cus(p->device) * nb);
   HIP_TRY(bote::launch_eval(a, n, true, grid, bd, shm, st));
   const hipMemcpyKind D2H = hipMemcpyDeviceToHost;
   if (out_vals) HIP_TRY(hipMemcpyAsync(out_vals, dvals.p, ncfg * stride * 4, D2H, st));
   if (out_leader) HIP_TRY(hipMemcpyAsync(out_leader, dlead.p, ncfg * 4, D2H, st));
-  if (out_sum) HIP_TRY(hipMemcpyAsync(out_sum, ds1.p, ncfg * bote::NSLOT * 8, D2H, st));
-  if (out_sumsq) HIP_TRY(hipMemcpyAsync(out_sumsq, ds2.p, ncfg * bote::NSLOT * 8, D2H, st));
-  if (out_mean) HIP_TRY(hipMemcpyAsync(out_mean, dmean.p, ncfg * bote::NSLOT * 8, D2H, st));
-  if (out_cov) HIP_TRY(hipMemcpyAsync(out_cov, dcov.p, ncfg * bote::NSLOT * 8, D2H, st));
+  if (out_sum) HIP_TRY(hipMemcpyAsync(out_sum, ds1.p, ncfg * NS * 8, D2H, st));
+  if (out_sumsq) HIP_TRY(hipMemcpyAsync(out_sumsq, ds2.p, ncfg * NS * 8, D2H, st));
+  if (out_mean) HIP_TRY(hipMemcpyAsync(out_mean, dmean.p, ncfg * NS * 8, D2H, st));
+  if (out_cov) HIP_TRY(hipMemcpyAsync(out_cov, dcov.p, ncfg * NS * 8, D2H, st));
+  if (keys && out_al_sum) HIP_TRY(hipMemcpyAsync(out_al_sum, dal1.p, nal * 8, D2H, st));
+  if (keys && out_al_sumsq) HIP_TRY(hipMemcpyAsync(out_al_sumsq, dal2.p, nal * 8, D2H, st));
   if (out_score && rp) HIP_TRY(hipMemcpyAsync(out_score, dscore.p, ncfg * 8, D2H, st));
   if (out_valid && rp) HIP_TRY(hipMemcpyAsync(out_valid, dvalid.p, ncfg, D2H, st));
   HIP_TRY(hipStreamSynchronize(st));
   return BOTE_OK;
+}
+
+int bote_eval(const bote_planet* p, const uint32_t* servers, uint32_t ns, const uint32_t* clients, uint32_t nc,
+              uint32_t n, const uint32_t* configs, uint64_t rank_begin, uint64_t ncfg, const bote_ranking_params* rp,
+              uint32_t* out_vals, uint32_t* out_leader, uint64_t* out_sum, uint64_t* out_sumsq, double* out_mean,
+              double* out_cov, double* out_score, uint8_t* out_valid) {
+  return eval_impl(p, servers, ns, clients, nc, n, configs, rank_begin, ncfg, rp, 0, out_vals, out_leader, out_sum,
+                   out_sumsq, out_mean, out_cov, out_score, out_valid, nullptr, nullptr);
+}
+
+int bote_eval_keys(const bote_planet* p, const uint32_t* servers, uint32_t ns, const uint32_t* clients, uint32_t nc,
+                   uint32_t n, const uint32_t* configs, uint64_t rank_begin, uint64_t ncfg, uint32_t keys,
+                   uint32_t* out_leader, uint64_t* out_sum, uint64_t* out_sumsq, uint64_t* out_al_sum,
+                   uint64_t* out_al_sumsq) {
+  return eval_impl(p, servers, ns, clients, nc, n, configs, rank_begin, ncfg, nullptr, keys, nullptr, out_leader,
+                   out_sum, out_sumsq, nullptr, nullptr, nullptr, nullptr, out_al_sum, out_al_sumsq);
 }
 
 // ------------------------------------------ leaderless, many quorum sizes
@@ -594,8 +619,28 @@ int bote_sweep_create(const bote_planet* p, const uint32_t* servers, uint32_t ns
 int bote_sweep_create_ex(const bote_planet* p, const uint32_t* servers, uint32_t ns, const uint32_t* clients,
                          uint32_t nc, uint32_t n, const bote_objective* objs, uint32_t n_obj, uint32_t K,
                          const bote_ranking_params* rp, int digest, int kernel, bote_sweep** out) {
+  return bote_sweep_create_keys(p, servers, ns, clients, nc, n, objs, n_obj, K, rp, digest, kernel, 0, out);
+}
+
+// slot s exists for config size n (f = 2 keys need max_f >= 2); slots >= 10
+// only with the extended key set
+static bool slot_exists_n(uint32_t n, uint32_t slot, uint32_t keys) {
+  const bool f2 = bote_max_f(n) >= 2;
+  if (slot < 10) {
+    const uint32_t b = slot % 5;
+    return !((b == BOTE_SLOT_AF2 || b == BOTE_SLOT_FF2) && !f2);
+  }
+  if (!keys || slot >= BOTE_NSLOTS_X) return false;
+  if (slot < 18) return (slot - 10) % 2 == 0 || f2;
+  return slot == 18 || f2;
+}
+
+int bote_sweep_create_keys(const bote_planet* p, const uint32_t* servers, uint32_t ns, const uint32_t* clients,
+                           uint32_t nc, uint32_t n, const bote_objective* objs, uint32_t n_obj, uint32_t K,
+                           const bote_ranking_params* rp, int digest, int kernel, uint32_t keys, bote_sweep** out) {
   int rc;
   if (!out) return fail(BOTE_E_ARG, "out is null");
+  if (keys > BOTE_KEYS_TEMPO_ALL_LEADERS) return fail(BOTE_E_ARG, "unknown key set");
   if (kernel < BOTE_KERNEL_AUTO || kernel > BOTE_KERNEL_GROUP) return fail(BOTE_E_ARG, "unknown kernel path");
   if ((rc = check_search_args(p, servers, ns, clients, nc, n))) return rc;
   if (n_obj > BOTE_MAX_OBJECTIVES) return fail(BOTE_E_RANGE, "more than 8 objectives");
@@ -608,10 +653,8 @@ int bote_sweep_create_ex(const bote_planet* p, const uint32_t* servers, uint32_t
       has_score = true;
       continue;
     }
-    if (objs[o].slot >= BOTE_NSLOTS) return fail(BOTE_E_ARG, "slot out of range");
-    uint32_t b = objs[o].slot % 5;
-    if ((b == BOTE_SLOT_AF2 || b == BOTE_SLOT_FF2) && bote_max_f(n) < 2)
-      return fail(BOTE_E_ARG, "slot does not exist for this n (max_f < 2)");
+    if (objs[o].slot >= (keys ? BOTE_NSLOTS_X : BOTE_NSLOTS)) return fail(BOTE_E_ARG, "slot out of range");
+    if (!slot_exists_n(n, objs[o].slot, keys)) return fail(BOTE_E_ARG, "slot does not exist for this n (max_f < 2)");
   }
   if (has_score && !rp) return fail(BOTE_E_ARG, "SCORE objective needs ranking params");
   if (rp && rp->ft_metric != BOTE_FT_F1 && rp->ft_metric != BOTE_FT_F1F2) return fail(BOTE_E_ARG, "bad ft_metric");
@@ -653,6 +696,7 @@ int bote_sweep_create_ex(const bote_planet* p, const uint32_t* servers, uint32_t
   }
   a.K = K;
   a.want_digest = digest ? 1 : 0;
+  a.keys = keys;
   a.out_counters = s->counters.as<unsigned long long>();
 
   s->bd = 256;
@@ -660,7 +704,7 @@ int bote_sweep_create_ex(const bote_planet* p, const uint32_t* servers, uint32_t
   s->shm = bote::eval_smem_bytes(a, n, s->bd, true);
   a.out_top = nullptr;
   if (s->shm > device_max_lds(p->device)) return cleanup(fail(BOTE_E_RANGE, "planet/client set too large for LDS"));
-  int nb = bote::eval_occupancy(n, false, s->bd, s->shm);
+  int nb = bote::eval_occupancy(n, false, s->bd, s->shm, keys != 0);
   s->grid = (uint32_t)(device_cus(p->device) * nb);
   s->xgrid = 32;
 
@@ -671,6 +715,33 @@ int bote_sweep_create_ex(const bote_planet* p, const uint32_t* servers, uint32_t
   s->fast = fast_eligible(p->lat.data(), p->R, servers, ns, nc, fair) && kernel != BOTE_KERNEL_GENERIC;
   if (kernel != BOTE_KERNEL_AUTO && kernel != BOTE_KERNEL_GENERIC && !s->fast)
     return cleanup(fail(BOTE_E_ARG, "the fast/group kernel is not eligible for this planet and lists"));
+  // the extended key set runs on the group kernel (n = 4..7, the default
+  // objectives first) or on the generic kernel
+  // (config 5's objective set, compiled into the group kernel: bote.py
+  // CONFIG5_OBJECTIVES = the default five, MEAN tt1, MEAN tw2, MEAN fl1)
+  bool keys_def = n_obj == 8 && has_score;
+  static const uint32_t dkk[8] = {BOTE_OBJ_SCORE, BOTE_OBJ_MEAN, BOTE_OBJ_MEAN, BOTE_OBJ_COV,
+                                  BOTE_OBJ_MEAN,  BOTE_OBJ_MEAN, BOTE_OBJ_MEAN, BOTE_OBJ_MEAN};
+  static const uint32_t dss[8] = {0, BOTE_SLOT_AF1, BOTE_SLOT_FF1, BOTE_SLOT_AF1,
+                                  BOTE_SLOT_E, BOTE_SLOT_TT1, BOTE_SLOT_TW2, BOTE_SLOT_FL1};
+  for (uint32_t o = 0; keys_def && o < 8; ++o)
+    keys_def = objs[o].kind == dkk[o] && (dkk[o] == BOTE_OBJ_SCORE || objs[o].slot == dss[o]);
+#ifndef BOTE_GROUP_BD
+#define BOTE_GROUP_BD 256
+#endif
+  // (the group kernel's extended keys use 32-bit moments: every sum of
+  // squares nc * (2 max)^2 and 3 nc max must fit their 32/24 bits)
+  uint64_t maxlat_all = 0;
+  for (auto v : p->lat) maxlat_all = std::max<uint64_t>(maxlat_all, v);
+  const bool keys32 = (uint64_t)nc * (2 * maxlat_all) * (2 * maxlat_all) < (1ull << 32) &&
+                      3ull * nc * maxlat_all < (1ull << 24);
+  if (keys && s->fast &&
+      (!bote::group_supports_keys(n, BOTE_GROUP_BD) || !keys_def || !keys32 || kernel == BOTE_KERNEL_FAST)) {
+    if (kernel == BOTE_KERNEL_FAST || kernel == BOTE_KERNEL_GROUP)
+      return cleanup(fail(BOTE_E_ARG, "the extended key set runs on the group kernel (n = 4..7, config 5's "
+                                      "objectives) or the generic kernel"));
+    s->fast = false;
+  }
   if (s->fast) {
     bote::FastArgs& f = s->fargs;
     f = bote::FastArgs{};
@@ -695,6 +766,7 @@ int bote_sweep_create_ex(const bote_planet* p, const uint32_t* servers, uint32_t
     f.rq_quads = cli_ident ? cq_quads : rq_quads;
     f.srv = s->srv.as<uint32_t>();
     f.ns = ns;
+    f.keys = keys;
     f.srv_identity = 1;
     for (uint32_t i = 0; i < ns; ++i) f.srv_identity &= servers[i] == i;
     f.nc = nc;
@@ -781,7 +853,7 @@ int bote_sweep_create_ex(const bote_planet* p, const uint32_t* servers, uint32_t
       // bote.py DEFAULT_OBJECTIVES: SCORE, MEAN af1, MEAN ff1, COV af1, MEAN e
       static const uint32_t dk[5] = {BOTE_OBJ_SCORE, BOTE_OBJ_MEAN, BOTE_OBJ_MEAN, BOTE_OBJ_COV, BOTE_OBJ_MEAN};
       static const uint32_t ds[5] = {0, BOTE_SLOT_AF1, BOTE_SLOT_FF1, BOTE_SLOT_AF1, BOTE_SLOT_E};
-      s->def_obj = n_obj == 5 && f.want_score;
+      s->def_obj = (keys ? keys_def : n_obj == 5) && f.want_score;
       for (uint32_t o = 0; s->def_obj && o < 5; ++o)
         s->def_obj = objs[o].kind == dk[o] && (dk[o] == BOTE_OBJ_SCORE || objs[o].slot == ds[o]);
       if (bote::group_uses_lines(n)) {
@@ -803,13 +875,15 @@ int bote_sweep_create_ex(const bote_planet* p, const uint32_t* servers, uint32_t
         }
       }
       const size_t gshm = bote::group_smem_bytes(f, n);
-      if (gshm <= device_max_lds(p->device)) {
+      if (gshm <= device_max_lds(p->device) && (!keys || s->def_obj)) {
         s->group = true;
         s->fshm = gshm;
         s->fgrid = (uint32_t)(device_cus(p->device) * std::max(1, bote::group_occupancy(f, n, gshm, s->def_obj)));
       }
     }
   }
+  // the fast (non-group) kernel does not compute the extended key set
+  if (keys && s->fast && !s->group) s->fast = false;
   // the generic path may also run on a fast sweep (overflow recompute)
   const uint32_t lists = s->fast ? std::max(s->grid, s->fgrid + s->xgrid) : s->grid;
   size_t top_bytes = (size_t)lists * std::max<uint32_t>(n_obj, 1) * bote::KP * 16;
@@ -1217,7 +1291,7 @@ int hip_fail(hipError_t e, const char* what) {
 int bote_search_create(const bote_planet* const* planets, uint32_t n_devices, const uint32_t* servers, uint32_t ns,
                        const uint32_t* clients, uint32_t nc, uint32_t n, uint64_t rank_begin, uint64_t rank_end,
                        const bote_objective* objs, uint32_t n_obj, uint32_t K, const bote_ranking_params* rp,
-                       int digest, bote_search** out) {
+                       int digest, uint32_t keys, bote_search** out) {
   if (!out) return fail(BOTE_E_ARG, "out is null");
   *out = nullptr;
   if (!planets || n_devices == 0) return fail(BOTE_E_ARG, "no planets");
@@ -1244,7 +1318,8 @@ int bote_search_create(const bote_planet* const* planets, uint32_t n_devices, co
   for (uint32_t i = 0; i < n_devices; ++i) {
     auto& x = h->sh[i];
     x.dev = planets[i]->device;
-    if ((rc = bote_sweep_create(planets[i], servers, ns, clients, nc, n, objs, n_obj, K, rp, digest, &x.sw)))
+    if ((rc = bote_sweep_create_keys(planets[i], servers, ns, clients, nc, n, objs, n_obj, K, rp, digest,
+                                     BOTE_KERNEL_AUTO, keys, &x.sw)))
       return cleanup(rc);
     if ((e = hipSetDevice(x.dev)) != hipSuccess) return cleanup(hip_fail(e, "hipSetDevice (shard)"));
     if ((e = hipStreamCreateWithFlags(&x.st, hipStreamNonBlocking)) != hipSuccess ||
@@ -1368,7 +1443,7 @@ int bote_search_topk(const bote_planet* const* planets, uint32_t n_devices, cons
                      uint64_t* out_digest) {
   bote_search* h = nullptr;
   int rc = bote_search_create(planets, n_devices, servers, ns, clients, nc, n, rank_begin, rank_end, objs, n_obj, K,
-                              rp, digest, &h);
+                              rp, digest, BOTE_KEYS_BASE, &h);
   if (rc) return rc;
   if (!(rc = bote_search_launch(h))) rc = bote_search_result(h, out, out_count, out_valid, out_digest);
   const std::string err = g_err;

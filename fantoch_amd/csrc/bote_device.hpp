@@ -37,6 +37,56 @@ struct QCfg {
   __host__ __device__ static constexpr int lq(int i) { return i == 0 ? lq0 : (i == 1 ? (a2_new ? qa2 : qe) : qe); }
 };
 
+// Leaderless quorum tables of a config of size N: the compute_stats q's
+// (QCfg::lq, tables 0 .. NL-1) and, with the extended key set (X: BASELINE
+// config 5, include/bote_hip.h BOTE_KEYS_TEMPO_ALL_LEADERS), Tempo's tiny fast
+// quorum 2f and write quorum f + 1 (fantoch/src/config.rs:317-329) where not
+// already among them, ascending (tables NL .. NT-1).
+template <int N, bool X>
+struct QTab {
+  using QC = QCfg<N>;
+  static constexpr bool base_has(int q) {
+    for (int t = 0; t < QC::NL; ++t)
+      if (QC::lq(t) == q) return true;
+    return false;
+  }
+  // Tempo's q's: f = 1: tiny 2, write 2; f = 2: tiny 4, write 3
+  static constexpr bool ext(int q) { return X && (q == 2 || (QC::maxf >= 2 && (q == 3 || q == 4))) && !base_has(q); }
+  static constexpr int NX = (ext(2) ? 1 : 0) + (ext(3) ? 1 : 0) + (ext(4) ? 1 : 0);
+  static constexpr int NT = QC::NL + NX;
+  __host__ __device__ static constexpr int q(int t) {
+    if (t < QC::NL) return QC::lq(t);
+    int k = t - QC::NL;
+    for (int qq = 2; qq <= 4; ++qq)
+      if (ext(qq)) {
+        if (k == 0) return qq;
+        --k;
+      }
+    return 0;
+  }
+  // table holding quorum size qq (-1: none)
+  __host__ __device__ static constexpr int idx(int qq) {
+    for (int t = 0; t < NT; ++t)
+      if (q(t) == qq) return t;
+    return -1;
+  }
+};
+
+// Slots of the extended key set (include/bote_hip.h): 10 + 4 * placement +
+// {tt1, tt2, tw1, tw2}; 18, 19 FPaxos under the best-by-mean leader (Input).
+constexpr int NSLOT_X = 20;
+enum { SLOT_TT1 = 10, SLOT_TT2 = 11, SLOT_TW1 = 12, SLOT_TW2 = 13, SLOT_FL1 = 18, SLOT_FL2 = 19 };
+// slot s exists for config size N (f = 2 keys need max_f >= 2)
+template <int N>
+__host__ __device__ constexpr bool slot_exists(int s) {
+  if (s < 10) {
+    const int b = s % 5;
+    return !((b == 2 || b == 3) && QCfg<N>::maxf < 2);
+  }
+  if (s < 18) return (s - 10) % 2 == 0 || QCfg<N>::maxf >= 2;  // tt2/tw2 (odd offsets) need f = 2
+  return s == 18 || QCfg<N>::maxf >= 2;
+}
+
 // ----------------------------------------------------------- small helpers
 __device__ __forceinline__ uint64_t mix64(uint64_t z) {
   z += 0x9E3779B97F4A7C15ull;
@@ -244,6 +294,13 @@ __device__ __forceinline__ uint32_t digest_fold(uint32_t h, uint64_t s1, uint64_
 }
 __device__ __forceinline__ uint64_t digest_final(uint64_t rank, uint32_t lead, uint32_t h) {
   return mix64(rank ^ ((uint64_t)lead << 56) ^ ((uint64_t)h << 24));
+}
+// The extended key set adds a second term per config: hx folds, from 0,
+// every leader's FPaxos moments (f = 1 then 2, leaders in config order), then
+// the present slots 18, 19, 14, 15, 16, 17, 10, 11, 12, 13 (the order the
+// group kernel produces them in).
+__device__ __forceinline__ uint64_t digest_final_x(uint64_t rank, uint32_t hx) {
+  return mix64(~rank ^ ((uint64_t)hx << 24));
 }
 
 // In-LDS bitonic sort of a[0..n), n a power of two, by the whole block.

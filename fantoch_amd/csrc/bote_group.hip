@@ -330,8 +330,26 @@ __device__ __forceinline__ float u64_to_f32(uint64_t x) {
 // regions in order (srv[p] == p), the digest is on and ft_metric is F1F2,
 // compiled in: the position -> region lookups and the flag tests vanish, and
 // with them uniform masks the kernel had spilled to VGPR lanes
-template <int N, bool DEF, bool SI, bool RXC>
-__global__ void __launch_bounds__(GROUP_MAX_BD, GCfg<N>::PERM ? BOTE_GROUP_WAVES_PERM : BOTE_GROUP_WAVES)
+// XK: the extended key set (BASELINE config 5: Tempo tiny/write keys and
+// every leader's FPaxos moments; include/bote_hip.h BOTE_KEYS_TEMPO_ALL_LEADERS)
+// on the PERM kernels, with config 5's objective set compiled in (the
+// default five, then MEAN tt1, MEAN tw2, MEAN fl1: bote.py CONFIG5_OBJECTIVES)
+// The extended key set keeps NT = 3..4 tables of byte planes and sums live
+// through the client loop: its kernels target 3 waves per SIMD (<= 168
+// VGPRs); config 5 (R = 128) is LDS-bound at 3 workgroups per CU anyway.
+// (a 1024-thread bound would cap registers at 128 whatever the wave target:
+// the XK kernels are bounded to 256-thread workgroups)
+#ifndef BOTE_GROUP_WAVES_XK
+#define BOTE_GROUP_WAVES_XK 3
+#endif
+constexpr uint32_t GROUP_XK_MAX_BD = 256;
+// client-loop quads per iteration of the base kernels (a build knob)
+#ifndef BOTE_GROUP_UNROLL
+#define BOTE_GROUP_UNROLL 4
+#endif
+template <int N, bool DEF, bool SI, bool RXC, bool XK>
+__global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
+                                  XK ? BOTE_GROUP_WAVES_XK : (GCfg<N>::PERM ? BOTE_GROUP_WAVES_PERM : BOTE_GROUP_WAVES))
     sweep_group_kernel(FastArgs a) {
   const bool sid = SI || a.srv_identity;
   // the position table: a launch argument, compiled in (RXC) on SI kernels
@@ -346,6 +364,9 @@ __global__ void __launch_bounds__(GROUP_MAX_BD, GCfg<N>::PERM ? BOTE_GROUP_WAVES
   constexpr int PV = Pow2<N - 1>::v;                 // variable row: N-1 values, padded
   constexpr int PF = Pow2<F>::v;                     // fixed-to-fixed row: F values (self = INF), padded
   constexpr bool PERM = GC::PERM;
+  static_assert(!XK || (PERM && DEF), "the extended key set runs on the PERM kernels with the default objectives");
+  using QT = QTab<N, XK>;
+  constexpr int NT = QT::NT;  // leaderless tables (PERM: register byte planes); == NL without XK
   extern __shared__ __align__(16) unsigned char smem[];
   size_t off[14];
   group_layout(a, N, NLW, KQ, PERM, off);
@@ -618,12 +639,12 @@ __global__ void __launch_bounds__(GROUP_MAX_BD, GCfg<N>::PERM ? BOTE_GROUP_WAVES
           // member m: 0..2 variable, 3.. fixed (config order = ascending positions)
           uint32_t Q2[N], Q3[N];
           uint32_t cS1p = 0, cS1e = 0;  // colocated sums: packed (t0 | t1 << 16), third table
-          uint32_t cS2[NL];
+          uint32_t cS2[NT], cS1t[NT];  // (PERM: per table)
 #pragma unroll
-          for (int t = 0; t < NL; ++t) cS2[t] = 0;
+          for (int t = 0; t < NT; ++t) cS2[t] = cS1t[t] = 0;
           // PERM: each table's member latencies as packed pair words, index
           // 0: members (0, 1), 1: member 2, 2 + pp: fixed members (3 + 2pp, 4 + 2pp)
-          uint32_t wp[2][2 + FP];
+          uint32_t wp[NT][2 + FP];
           // sorted row (packed pair: lo = member j, hi = member j + 1)
           auto emit_pk = [&](int j, bool has_hi, const uint32_t* L) {
             const uint32_t w0 = L[QC::lq(0) - 2], w1 = L[(NL >= 2 ? QC::lq(1) : QC::lq(0)) - 2];
@@ -636,8 +657,10 @@ __global__ void __launch_bounds__(GROUP_MAX_BD, GCfg<N>::PERM ? BOTE_GROUP_WAVES
               }
               const int pi = j == 0 ? 0 : (j == 2 ? 1 : 2 + (j - 3) / 2);
               const uint32_t hm = has_hi ? ~0u : 0xFFFFu;
-              wp[0][pi] = w0 & hm;
-              wp[1][pi] = w1 & hm;
+#pragma unroll
+              for (int t = 0; t < NT; ++t) wp[t][pi] = L[QT::q(t) - 2] & hm;
+              (void)w0;
+              (void)w1;
               return;
             }
 #pragma unroll
@@ -825,10 +848,10 @@ __global__ void __launch_bounds__(GROUP_MAX_BD, GCfg<N>::PERM ? BOTE_GROUP_WAVES
           // ---- PERM: byte planes (member m's latency: low byte in byte m of
           //      QL, high byte in byte m of QH; members 0..3 in .x, 4..6 in
           //      .y) and the colocated sums over the members
-          uint2 QL[2], QH[2];
+          uint2 QL[NT], QH[NT];
           if constexpr (PERM) {
 #pragma unroll
-            for (int t = 0; t < 2; ++t) {
+            for (int t = 0; t < NT; ++t) {
               const uint32_t w01 = wp[t][0], w2 = wp[t][1], w34 = wp[t][2], w56 = FP >= 2 ? wp[t][FP >= 2 ? 3 : 2] : 0u;
               QL[t].x = __builtin_amdgcn_perm(w2, w01, 0x0C040200u) | (w34 << 24);
               QH[t].x = __builtin_amdgcn_perm(w34, __builtin_amdgcn_perm(w2, w01, 0x0C050301u), 0x05020100u);
@@ -841,7 +864,7 @@ __global__ void __launch_bounds__(GROUP_MAX_BD, GCfg<N>::PERM ? BOTE_GROUP_WAVES
                 sq = __builtin_amdgcn_udot2(as_us2(wp[t][i]), as_us2(wp[t][i]), sq, false);
               }
               cS2[t] = sq;
-              cS1p |= ((ps & 0xFFFFu) + (ps >> 16)) << (16 * t);
+              cS1t[t] = (ps & 0xFFFFu) + (ps >> 16);
             }
           }
           // ---- FPaxos leader (f = 1, q = 2, min COV, first in config order)
@@ -918,16 +941,65 @@ __global__ void __launch_bounds__(GROUP_MAX_BD, GCfg<N>::PERM ? BOTE_GROUP_WAVES
                 lreg = reg_of(l);
               }
             Mom mom[NSLOT];
+            // XK: the extended slots and every leader's FPaxos moments are
+            // folded into their own digest word as they are produced
+            // (digest_final_x: the leaders, slots 18-19, 14-17, 10-13), so
+            // none stays live to the end of the config; objectives 5..7 keep
+            // one sum each (tt1, tw2, fl1)
+            uint32_t hx = 0;
+            uint32_t x_tt1 = 0, x_tw2 = 0, x_fl1 = 0;
+            auto xslot = [&](uint64_t s1, uint64_t s2) { hx = digest_fold(hx, s1, s2); };
+            (void)xslot;
+            // ---- XK, before the client loop (so that none of it stays live
+            //      through it): FPaxos all leaders (Bote::all_leaders_stats, lib.rs:129-150)
+            //      over the Input clients at q = f + 1, members in config
+            //      order, from the column sums (closed form, as ff1/ff2); the
+            //      digest consumes every one, and slots fl1/fl2 take the best
+            //      leader by Stats::Mean (lib.rs:99-121: the first minimum)
+            if constexpr (XK) {
+              // 32-bit arithmetic: the host runs XK here only when every sum
+              // of squares fits (nc * (2 * max latency)^2 < 2^32), so
+              // S2 = c2 + q (c1 + S1) with 24-bit multiplies (c1, S1 < 2^24)
+              uint32_t b1 = ~0u, b2 = ~0u, b1s = 0, b2s = 0;
+#pragma unroll
+              for (int f = 0; f < 2; ++f) {
+#pragma unroll
+                for (int l = 0; l < N; ++l) {
+                  const uint32_t c1 = s1_of(l), c2 = (uint32_t)cs2[pos_of(l)];
+                  const uint32_t q = f == 0 ? Q2[l] : Q3[l];
+                  const uint32_t m1 = __umul24(nc, q) + c1;  // (nc, q, c1 + m1 < 2^24)
+                  const uint32_t m2 = __umul24(q, c1 + m1) + c2;
+                  hx = digest_fold(hx, m1, m2);
+                  if (f == 0 && m1 < b1) {
+                    b1 = m1;
+                    b1s = m2;
+                  }
+                  if (f == 1 && m1 < b2) {
+                    b2 = m1;
+                    b2s = m2;
+                  }
+                }
+              }
+              xslot(b1, b1s);  // slot 18 (fl1)
+              xslot(b2, b2s);  // slot 19 (fl2)
+              x_fl1 = (uint32_t)b1;
+              // Colocated Tempo: the members' own quorum latencies (slots 14..17)
+              constexpr int t2 = QT::idx(2), t3 = QT::idx(3), t4 = QT::idx(4);
+              xslot(cS1t[t2], cS2[t2]);
+              xslot(cS1t[t4], cS2[t4]);
+              xslot(cS1t[t2], cS2[t2]);
+              xslot(cS1t[t3], cS2[t3]);
+            }
             // ---- Input leaderless: 3 lane columns + the wave's nearest-fixed line
             {
               const us2 J1 = {1, 1}, J2 = {2, 2};
               // Sums use full-rate 32-bit adds on packed u16 pairs (no half
               // overflows: lat + q < 2^15, and p1 is flushed every g_flush
               // quads), squares the 2-wide dot product (s2, flushed to 64 bits)
-              uint32_t S1[NL], s2[NL], p1[NL];
-              uint64_t S2[NL];
+              uint32_t S1[NT], s2[NT], p1[NT];
+              uint64_t S2[NT];
 #pragma unroll
-              for (int t = 0; t < NL; ++t) {
+              for (int t = 0; t < NT; ++t) {
                 S1[t] = 0;
                 S2[t] = 0;
                 s2[t] = 0;
@@ -980,7 +1052,7 @@ __global__ void __launch_bounds__(GROUP_MAX_BD, GCfg<N>::PERM ? BOTE_GROUP_WAVES
                   // (v_perm over the byte planes), interleaved into u16 pairs
                   const uint32_t sel = __builtin_amdgcn_perm(H, L, 0x06040200u) & 0x0F0F0F0Fu;
 #pragma unroll
-                  for (int t = 0; t < 2; ++t) {
+                  for (int t = 0; t < NT; ++t) {
                     const uint32_t bl = __builtin_amdgcn_perm(QL[t].y, QL[t].x, sel);
                     const uint32_t bh = __builtin_amdgcn_perm(QH[t].y, QH[t].x, sel);
                     acc1(t, as_us2(__builtin_amdgcn_perm(bh, bl, 0x05010400u)),
@@ -1009,7 +1081,7 @@ __global__ void __launch_bounds__(GROUP_MAX_BD, GCfg<N>::PERM ? BOTE_GROUP_WAVES
               };
               auto flush = [&]() {
 #pragma unroll
-                for (int t = 0; t < NL; ++t) {
+                for (int t = 0; t < NT; ++t) {
                   S2[t] += s2[t];
                   s2[t] = 0;
                   S1[t] += (p1[t] & 0xFFFFu) + (p1[t] >> 16);
@@ -1019,16 +1091,17 @@ __global__ void __launch_bounds__(GROUP_MAX_BD, GCfg<N>::PERM ? BOTE_GROUP_WAVES
               const uint32_t nql = ABLATE(a, 1) ? 0u : nq;
               // 4 quads per iteration (constant offsets fold into the ds_read
               // offset fields); s2 is flushed to 64 bits every s2_flush quads
+              // (XK: 2 quads per iteration; its 4 tables' temporaries of 4
+              // unrolled quads spill)
+              constexpr uint32_t U = XK ? 2u : (uint32_t)BOTE_GROUP_UNROLL;
               auto clients = [&](auto lines_c) {
-                const uint32_t f4 = a.g_flush >> 2 ? a.g_flush >> 2 : 1u;
+                const uint32_t fU = a.g_flush / U ? a.g_flush / U : 1u;
                 uint32_t g = 0, k = 0;
-                if (a.g_flush >= 4) {
-                  for (; g + 4 <= nql; g += 4) {
-                    quad(lines_c, g * 8, ~0u, ~0u);
-                    quad(lines_c, g * 8 + 8, ~0u, ~0u);
-                    quad(lines_c, g * 8 + 16, ~0u, ~0u);
-                    quad(lines_c, g * 8 + 24, ~0u, ~0u);
-                    if (++k == f4) {
+                if (a.g_flush >= U) {
+                  for (; g + U <= nql; g += U) {
+#pragma unroll
+                    for (uint32_t u = 0; u < U; ++u) quad(lines_c, g * 8 + 8 * u, ~0u, ~0u);
+                    if (++k == fU) {
                       flush();
                       k = 0;
                     }
@@ -1049,7 +1122,7 @@ __global__ void __launch_bounds__(GROUP_MAX_BD, GCfg<N>::PERM ? BOTE_GROUP_WAVES
               else clients(BoolC<false>{});
               if (ABLATE(a, 1)) {  // timing only: non-degenerate dummy sums
 #pragma unroll
-                for (int t = 0; t < NL; ++t) {
+                for (int t = 0; t < NT; ++t) {
                   S1[t] = 1000u + rv[0] + t;
                   S2[t] = (uint64_t)S1[t] * S1[t] + 12345u;
                 }
@@ -1057,6 +1130,16 @@ __global__ void __launch_bounds__(GROUP_MAX_BD, GCfg<N>::PERM ? BOTE_GROUP_WAVES
               mom[SLOT_AF1] = Mom{S1[QC::idx_a1], S2[QC::idx_a1], nc};
               mom[SLOT_AF2] = Mom{S1[QC::idx_a2], S2[QC::idx_a2], nc};
               mom[SLOT_E] = Mom{S1[QC::idx_e], S2[QC::idx_e], nc};
+              if constexpr (XK) {
+                // Tempo tiny (2f) and write (f + 1) quorums, Input: slots 10..13
+                constexpr int t2 = QT::idx(2), t3 = QT::idx(3), t4 = QT::idx(4);
+                xslot(S1[t2], S2[t2]);  // slot 10 (tt1)
+                xslot(S1[t4], S2[t4]);  // slot 11 (tt2)
+                xslot(S1[t2], S2[t2]);  // slot 12 (tw1)
+                xslot(S1[t3], S2[t3]);  // slot 13 (tw2)
+                x_tt1 = S1[t2];
+                x_tw2 = S1[t3];
+              }
             }
             // ---- Input FPaxos from the leader column's sums
             const uint32_t lc1 = lrec[lpos].x;
@@ -1080,7 +1163,15 @@ __global__ void __launch_bounds__(GROUP_MAX_BD, GCfg<N>::PERM ? BOTE_GROUP_WAVES
               const uint32_t f1s = sv2 + 2 * lq2 * sv + N * lq2 * lq2, f2s = sv2 + 2 * lq3 * sv + N * lq3 * lq3;
               mom[5 + SLOT_FF1] = Mom{f1, f1s, (uint32_t)N};
               mom[5 + SLOT_FF2] = Mom{f2, f2s, (uint32_t)N};
-              const uint32_t cl1[3] = {cS1p & 0xFFFFu, cS1p >> 16, cS1e};
+              uint32_t cl1[NT > 3 ? NT : 3];
+              if constexpr (PERM) {
+#pragma unroll
+                for (int t = 0; t < NT; ++t) cl1[t] = cS1t[t];
+              } else {
+                cl1[0] = cS1p & 0xFFFFu;
+                cl1[1] = cS1p >> 16;
+                cl1[2] = cS1e;
+              }
               mom[5 + SLOT_AF1] = Mom{cl1[QC::idx_a1], cS2[QC::idx_a1], (uint32_t)N};
               mom[5 + SLOT_AF2] = Mom{cl1[QC::idx_a2], cS2[QC::idx_a2], (uint32_t)N};
               mom[5 + SLOT_E] = Mom{cl1[QC::idx_e], cS2[QC::idx_e], (uint32_t)N};
@@ -1095,7 +1186,7 @@ __global__ void __launch_bounds__(GROUP_MAX_BD, GCfg<N>::PERM ? BOTE_GROUP_WAVES
             };
             const uint64_t Va1 = mom_v32(mom[SLOT_AF1]);
             const float va1 = u64_to_f32(Va1);
-            if (DEF) {
+            if constexpr (DEF) {
               // ---- compute_score validity (search.rs:421-472), exact.  The
               //      integer mean tests of every f first; the COV tests only
               //      for configs that pass them, and a config is deferred
@@ -1153,6 +1244,7 @@ __global__ void __launch_bounds__(GROUP_MAX_BD, GCfg<N>::PERM ? BOTE_GROUP_WAVES
 #pragma unroll
                   for (int sl = 0; sl < NSLOT; ++sl) h = digest_fold(h, mom[sl].s1, mom[sl].s2);
                   digest += digest_final(rank, bi, h);
+                  if constexpr (XK) digest += digest_final_x(rank, hx);
                 }
                 // ---- default objectives: 0 SCORE, 1 MEAN af1, 2 MEAN ff1, 3 COV af1, 4 MEAN e
                 if (ABLATE(a, 2048)) valid = false;
@@ -1160,6 +1252,12 @@ __global__ void __launch_bounds__(GROUP_MAX_BD, GCfg<N>::PERM ? BOTE_GROUP_WAVES
                 key[1] = mom[SLOT_AF1].s1;
                 key[2] = mom[SLOT_FF1].s1;
                 key[4] = mom[SLOT_E].s1;
+                if constexpr (XK) {  // 5 MEAN tt1, 6 MEAN tw2, 7 MEAN fl1
+                  ok[5] = ok[6] = ok[7] = true;
+                  key[5] = x_tt1;
+                  key[6] = x_tw2;
+                  key[7] = x_fl1;
+                }
                 if (valid) {
                   const uint64_t tkey = tk.thr[0].key;
                   bool maybe = tkey == ~0ull;
@@ -1217,7 +1315,7 @@ __global__ void __launch_bounds__(GROUP_MAX_BD, GCfg<N>::PERM ? BOTE_GROUP_WAVES
         }
         // ---- top-K: lock-free screen, exact merge under the block lock
         if (!ABLATE(a, 4)) {
-          const int nobj = DEF ? 5 : a.n_obj;
+          const int nobj = XK ? 8 : (DEF ? 5 : a.n_obj);
           bool pass = false;
 #pragma unroll
           for (int o = 0; o < MAXOBJ; ++o)
@@ -1262,9 +1360,9 @@ __global__ void __launch_bounds__(GROUP_MAX_BD, GCfg<N>::PERM ? BOTE_GROUP_WAVES
 }
 
 // ------------------------------------------------------------- launcher ---
-template <int N, bool DEF, bool SI, bool RXC>
+template <int N, bool DEF, bool SI, bool RXC, bool XK>
 static hipError_t launch_group_n(const FastArgs& a, uint32_t grid, size_t shm, hipStream_t st) {
-  auto k = sweep_group_kernel<N, DEF, SI, RXC>;
+  auto k = sweep_group_kernel<N, DEF, SI, RXC, XK>;
   hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k, dim3(grid), dim3(a.gbd), shm, st, a);
@@ -1274,17 +1372,46 @@ static hipError_t launch_group_n(const FastArgs& a, uint32_t grid, size_t shm, h
 // The instantiation launch_group runs for these arguments (its occupancy
 // decides the persistent grid, so it must be the kernel that runs).
 static bool group_si(const FastArgs& a) { return a.srv_identity && a.want_digest && a.ft_metric == 2; }
+
+// the extended key set: PERM kernels (n = 4..7) with the default objectives
+bool group_supports_keys(uint32_t n, uint32_t bd) { return n >= 4 && n <= 7 && group_uses_lines(n) && bd <= GROUP_XK_MAX_BD; }
+
+template <int N, bool XK>
+static const void* group_fn_n(const FastArgs& a, bool def) {
+  if constexpr (XK) {
+    return group_si(a) ? (a.grx ? (const void*)sweep_group_kernel<N, true, true, true, true>
+                                : (const void*)sweep_group_kernel<N, true, true, false, true>)
+                       : (const void*)sweep_group_kernel<N, true, false, false, true>;
+  } else {
+    return def ? (group_si(a) ? (a.grx ? (const void*)sweep_group_kernel<N, true, true, true, false>
+                                       : (const void*)sweep_group_kernel<N, true, true, false, false>)
+                              : (const void*)sweep_group_kernel<N, true, false, false, false>)
+               : (const void*)sweep_group_kernel<N, false, false, false, false>;
+  }
+}
+
+template <int N, bool XK>
+static hipError_t launch_group_x(const FastArgs& a, bool def, uint32_t grid, size_t shm, hipStream_t st) {
+  if constexpr (XK) {
+    return group_si(a) ? (a.grx ? launch_group_n<N, true, true, true, true>(a, grid, shm, st)
+                                : launch_group_n<N, true, true, false, true>(a, grid, shm, st))
+                       : launch_group_n<N, true, false, false, true>(a, grid, shm, st);
+  } else {
+    return def ? (group_si(a) ? (a.grx ? launch_group_n<N, true, true, true, false>(a, grid, shm, st)
+                                       : launch_group_n<N, true, true, false, false>(a, grid, shm, st))
+                              : launch_group_n<N, true, false, false, false>(a, grid, shm, st))
+               : launch_group_n<N, false, false, false, false>(a, grid, shm, st);
+  }
+}
+
 static const void* group_fn(const FastArgs& a, uint32_t n, bool def) {
   switch (n) {
-#define FN_CASE(NN)                                                                                       \
-  case NN:                                                                                                \
-    return def ? (group_si(a) ? (a.grx ? (const void*)sweep_group_kernel<NN, true, true, true>            \
-                                       : (const void*)sweep_group_kernel<NN, true, true, false>)          \
-                              : (const void*)sweep_group_kernel<NN, true, false, false>)                  \
-               : (const void*)sweep_group_kernel<NN, false, false, false>;
-    FN_CASE(4) FN_CASE(5) FN_CASE(6) FN_CASE(7) FN_CASE(8) FN_CASE(9) FN_CASE(10) FN_CASE(11) FN_CASE(12)
-    FN_CASE(13) FN_CASE(14) FN_CASE(15) FN_CASE(16)
+#define FN_CASE(NN) case NN: return a.keys ? group_fn_n<NN, true>(a, def) : group_fn_n<NN, false>(a, def);
+#define FN_CASE0(NN) case NN: return a.keys ? nullptr : group_fn_n<NN, false>(a, def);
+    FN_CASE(4) FN_CASE(5) FN_CASE(6) FN_CASE(7) FN_CASE0(8) FN_CASE0(9) FN_CASE0(10) FN_CASE0(11) FN_CASE0(12)
+    FN_CASE0(13) FN_CASE0(14) FN_CASE0(15) FN_CASE0(16)
 #undef FN_CASE
+#undef FN_CASE0
     default: return nullptr;
   }
 }
@@ -1301,15 +1428,13 @@ int group_occupancy(const FastArgs& a, uint32_t n, size_t shm, bool def) {
 hipError_t launch_group(const FastArgs& a, uint32_t n, bool def, uint32_t grid, size_t shm, hipStream_t st) {
   switch (n) {
 #define GS_CASE(NN) \
-  case NN:                                                                                           \
-    return def ? (group_si(a)                                                                        \
-                      ? (a.grx ? launch_group_n<NN, true, true, true>(a, grid, shm, st)              \
-                               : launch_group_n<NN, true, true, false>(a, grid, shm, st))             \
-                      : launch_group_n<NN, true, false, false>(a, grid, shm, st))                    \
-               : launch_group_n<NN, false, false, false>(a, grid, shm, st);
-    GS_CASE(4) GS_CASE(5) GS_CASE(6) GS_CASE(7) GS_CASE(8) GS_CASE(9) GS_CASE(10) GS_CASE(11) GS_CASE(12)
-    GS_CASE(13) GS_CASE(14) GS_CASE(15) GS_CASE(16)
+  case NN: return a.keys ? launch_group_x<NN, true>(a, def, grid, shm, st) : launch_group_x<NN, false>(a, def, grid, shm, st);
+#define GS_CASE0(NN) \
+  case NN: return a.keys ? hipErrorInvalidValue : launch_group_x<NN, false>(a, def, grid, shm, st);
+    GS_CASE(4) GS_CASE(5) GS_CASE(6) GS_CASE(7) GS_CASE0(8) GS_CASE0(9) GS_CASE0(10) GS_CASE0(11) GS_CASE0(12)
+    GS_CASE0(13) GS_CASE0(14) GS_CASE0(15) GS_CASE0(16)
 #undef GS_CASE
+#undef GS_CASE0
     default: return hipErrorInvalidValue;
   }
 }

@@ -85,8 +85,13 @@ __device__ __forceinline__ uint32_t sel(const uint32_t (&arr)[N], uint32_t i) {
 }
 
 // --------------------------------------------------------- config result --
+// X: the extended key set (slots 10..19 and every leader's FPaxos moments,
+// al[f - 1][config-order leader], Input clients)
+template <int N, bool X>
 struct CfgOut {
-  Mom mom[NSLOT];
+  static constexpr int NS = X ? NSLOT_X : NSLOT;
+  Mom mom[NS];
+  Mom al[X ? 2 : 1][X ? N : 1];
   uint32_t lead_orig;
   double score;
   bool valid;
@@ -95,18 +100,19 @@ struct CfgOut {
 // Slot presence for a config of size N (af2/ff2 need max_f >= 2).
 template <int N>
 __device__ __forceinline__ bool slot_has(int s) {
-  int b = s % 5;
-  return !((b == SLOT_AF2 || b == SLOT_FF2) && QCfg<N>::maxf < 2);
+  return slot_exists<N>(s);
 }
 
 // ------------------------------------------------------------- eval one ---
 // Evaluate the configuration whose members are positions p[0..N) of the
 // server list (given order = config order).  `oi` is the output row (FULL).
-template <int N, bool FULL>
+template <int N, bool FULL, bool X>
 __device__ __forceinline__ void eval_config(const EvalArgs& a, const Smem& s, const uint32_t (&p)[N], bool sorted_in, uint64_t oi,
-                            CfgOut& out) {
+                            CfgOut<N, X>& out) {
   using QC = QCfg<N>;
-  constexpr int NL = QC::NL;
+  using QT = QTab<N, X>;
+  constexpr int NL = QT::NT;  // leaderless tables: compute_stats' q's, then the extended ones
+  constexpr int NLW = (NL + 1) / 2;
   constexpr int P = Pow2<N>::v;
   const uint32_t BD = blockDim.x, tid = threadIdx.x;
   const uint32_t R = a.R, nc = a.nc;
@@ -147,17 +153,13 @@ __device__ __forceinline__ void eval_config(const EvalArgs& a, const Smem& s, co
     Qf1[j] = v[QC::qf1 - 1];
     Qf2[j] = QC::maxf >= 2 ? v[(QC::maxf >= 2 ? QC::qf2 : 1) - 1] : 0;
 #pragma unroll
-    for (int t = 0; t < NL; ++t) Ql[t][j] = v[QC::lq(t) - 1];
+    for (int t = 0; t < NL; ++t) Ql[t][j] = v[QT::q(t) - 1];
     cdk[j] = key;
-    if (NL <= 2) {
-      uint32_t w = Ql[0][j] | (NL == 2 ? (Ql[NL - 1][j] << 16) : 0u);
-      s.qtab[j * BD + tid] = w;
-    } else {
-      uint2 w;
-      w.x = Ql[0][j] | (Ql[1][j] << 16);
-      w.y = Ql[NL - 1][j];
-      ((uint2*)s.qtab)[j * BD + tid] = w;
-    }
+    // the lane's quorum tables, two u16 per word: word w of member j at
+    // qtab[(j * NLW + w) * BD + tid] (bank-conflict free)
+#pragma unroll
+    for (int w = 0; w < NLW; ++w)
+      s.qtab[(j * NLW + w) * BD + tid] = Ql[2 * w][j] | (2 * w + 1 < NL ? (Ql[2 * w + 1 < NL ? 2 * w + 1 : 0][j] << 16) : 0u);
   }
 
   // --- FPaxos leader: min COV over the Input clients at f = 1 (q = 2),
@@ -257,6 +259,13 @@ __device__ __forceinline__ void eval_config(const EvalArgs& a, const Smem& s, co
     out.mom[5 + SLOT_AF1] = Mom{l1[QC::idx_a1], l2[QC::idx_a1], (uint32_t)N};
     out.mom[5 + SLOT_AF2] = Mom{l1[QC::idx_a2], l2[QC::idx_a2], (uint32_t)N};
     out.mom[5 + SLOT_E] = Mom{l1[QC::idx_e], l2[QC::idx_e], (uint32_t)N};
+    if constexpr (X) {
+      constexpr int t2 = QT::idx(2), t3 = QT::idx(3) < 0 ? 0 : QT::idx(3), t4 = QT::idx(4) < 0 ? 0 : QT::idx(4);
+      out.mom[4 + SLOT_TT1] = Mom{l1[t2], l2[t2], (uint32_t)N};
+      out.mom[4 + SLOT_TW1] = Mom{l1[t2], l2[t2], (uint32_t)N};
+      out.mom[4 + SLOT_TT2] = Mom{l1[t4], l2[t4], (uint32_t)N};
+      out.mom[4 + SLOT_TW2] = Mom{l1[t3], l2[t3], (uint32_t)N};
+    }
   }
 
   // --- Input leaderless: the hot loop.  Per client (wave-uniform): the
@@ -274,15 +283,11 @@ __device__ __forceinline__ void eval_config(const EvalArgs& a, const Smem& s, co
       for (int k = 0; k < N; ++k) m = min(m, s.mat[off + mreg[k]] | (uint32_t)k);
       const uint32_t js = m & 15, d = m >> LAT_SHIFT;
       uint32_t A[NL];
-      if (NL <= 2) {
-        uint32_t w = s.qtab[js * BD + tid];
-        A[0] = d + (w & 0xFFFF);
-        if (NL == 2) A[NL - 1] = d + (w >> 16);
-      } else {
-        uint2 w = ((const uint2*)s.qtab)[js * BD + tid];
-        A[0] = d + (w.x & 0xFFFF);
-        A[1] = d + (w.x >> 16);
-        A[NL - 1] = d + w.y;
+#pragma unroll
+      for (int w = 0; w < NLW; ++w) {
+        const uint32_t wd = s.qtab[(js * NLW + w) * BD + tid];
+        A[2 * w] = d + (wd & 0xFFFF);
+        if (2 * w + 1 < NL) A[2 * w + 1 < NL ? 2 * w + 1 : 0] = d + (wd >> 16);
       }
 #pragma unroll
       for (int t = 0; t < NL; ++t) {
@@ -301,6 +306,38 @@ __device__ __forceinline__ void eval_config(const EvalArgs& a, const Smem& s, co
     out.mom[SLOT_AF1] = Mom{S1[QC::idx_a1], S2[QC::idx_a1], nc};
     out.mom[SLOT_AF2] = Mom{S1[QC::idx_a2], S2[QC::idx_a2], nc};
     out.mom[SLOT_E] = Mom{S1[QC::idx_e], S2[QC::idx_e], nc};
+    if constexpr (X) {
+      // Tempo tiny (2f) and write (f + 1) quorums, Input
+      constexpr int t2 = QT::idx(2), t3 = QT::idx(3) < 0 ? 0 : QT::idx(3), t4 = QT::idx(4) < 0 ? 0 : QT::idx(4);
+      out.mom[SLOT_TT1] = Mom{S1[t2], S2[t2], nc};
+      out.mom[SLOT_TW1] = Mom{S1[t2], S2[t2], nc};
+      out.mom[SLOT_TT2] = Mom{S1[t4], S2[t4], nc};
+      out.mom[SLOT_TW2] = Mom{S1[t3], S2[t3], nc};
+    }
+  }
+  if constexpr (X) {
+    // FPaxos all leaders (Bote::all_leaders_stats, lib.rs:129-150), Input
+    // clients, q = f + 1, leaders in config order, and the best leader by
+    // Stats::Mean (lib.rs:99-121: the first minimum, exact sums)
+#pragma unroll
+    for (int o = 0; o < N; ++o) {
+      uint32_t l = 0;
+#pragma unroll
+      for (int k = 0; k < N; ++k) l = morig[k] == (uint32_t)o ? (uint32_t)k : l;
+      const uint32_t pl = sel(mpos, l);
+      const uint64_t c1 = s.cs[2 * pl], c2 = s.cs[2 * pl + 1];
+      const uint64_t q1 = sel(Qf1, l), q2 = sel(Qf2, l);
+      out.al[0][o] = Mom{c1 + (uint64_t)nc * q1, c2 + 2ull * q1 * c1 + (uint64_t)nc * q1 * q1, nc};
+      out.al[1][o] = Mom{c1 + (uint64_t)nc * q2, c2 + 2ull * q2 * c1 + (uint64_t)nc * q2 * q2, nc};
+    }
+    Mom b1 = out.al[0][0], b2 = out.al[1][0];
+#pragma unroll
+    for (int o = 1; o < N; ++o) {
+      if (out.al[0][o].s1 < b1.s1) b1 = out.al[0][o];
+      if (out.al[1][o].s1 < b2.s1) b2 = out.al[1][o];
+    }
+    out.mom[SLOT_FL1] = b1;
+    out.mom[SLOT_FL2] = b2;
   }
 
   // --- Search::compute_score (search.rs:421-472), bit-exact.
@@ -365,10 +402,10 @@ __device__ __forceinline__ void eval_config(const EvalArgs& a, const Smem& s, co
 }
 
 // ------------------------------------------------------------ the kernel --
-template <int N, bool FULL>
+template <int N, bool FULL, bool X>
 __global__ void __launch_bounds__(256) eval_kernel(EvalArgs a) {
-  using QC = QCfg<N>;
-  constexpr int NLW = QC::NL <= 2 ? 1 : 2;
+  constexpr int NLW = (QTab<N, X>::NT + 1) / 2;
+  constexpr int NS = CfgOut<N, X>::NS;
   extern __shared__ __align__(16) unsigned char smem[];
   if (a.run_if_over && *a.run_if_over <= a.over_cap) return;  // block-uniform, before any barrier
   const Smem s = carve<N>(a, smem, NLW);
@@ -430,9 +467,9 @@ __global__ void __launch_bounds__(256) eval_kernel(EvalArgs a) {
     }
     for (uint64_t t = 0; t < runlen; ++t) {
       const bool have = jobok && rank < rend;
-      CfgOut r;
+      CfgOut<N, X> r;
       if (have) {
-        eval_config<N, FULL>(a, s, p, sorted_in, rank - a.rb, r);
+        eval_config<N, FULL, X>(a, s, p, sorted_in, rank - a.rb, r);
         if (r.valid) ++valid_cnt;
         if (a.want_digest) {
           uint32_t h = 0;
@@ -440,17 +477,42 @@ __global__ void __launch_bounds__(256) eval_kernel(EvalArgs a) {
           for (int sl = 0; sl < NSLOT; ++sl)
             if (slot_has<N>(sl)) h = digest_fold(h, r.mom[sl].s1, r.mom[sl].s2);
           digest += digest_final(rank, r.lead_orig, h);
+          if constexpr (X) {
+            // (the order of digest_final_x: all leaders, 18-19, 14-17, 10-13)
+            uint32_t hx = 0;
+#pragma unroll
+            for (int f = 0; f < 2; ++f) {
+              if (f >= QCfg<N>::maxf) break;
+#pragma unroll
+              for (int l = 0; l < N; ++l) hx = digest_fold(hx, r.al[f][l].s1, r.al[f][l].s2);
+            }
+            constexpr int order[10] = {18, 19, 14, 15, 16, 17, 10, 11, 12, 13};
+#pragma unroll
+            for (int i = 0; i < 10; ++i)
+              if (slot_has<N>(order[i])) hx = digest_fold(hx, r.mom[order[i]].s1, r.mom[order[i]].s2);
+            digest += digest_final_x(rank, hx);
+          }
         }
         if (FULL) {
           const uint64_t oi = rank - a.rb;
           if (a.out_leader) a.out_leader[oi] = r.lead_orig;
 #pragma unroll
-          for (int sl = 0; sl < NSLOT; ++sl) {
+          for (int sl = 0; sl < NS; ++sl) {
             const bool h = slot_has<N>(sl);
-            if (a.out_s1) a.out_s1[oi * NSLOT + sl] = h ? r.mom[sl].s1 : ~0ull;
-            if (a.out_s2) a.out_s2[oi * NSLOT + sl] = h ? r.mom[sl].s2 : ~0ull;
-            if (a.out_mean) a.out_mean[oi * NSLOT + sl] = h ? mom_mean(r.mom[sl]) : __longlong_as_double(0x7FF8000000000000ll);
-            if (a.out_cov) a.out_cov[oi * NSLOT + sl] = h ? mom_cov(r.mom[sl]) : __longlong_as_double(0x7FF8000000000000ll);
+            if (a.out_s1) a.out_s1[oi * NS + sl] = h ? r.mom[sl].s1 : ~0ull;
+            if (a.out_s2) a.out_s2[oi * NS + sl] = h ? r.mom[sl].s2 : ~0ull;
+            if (a.out_mean) a.out_mean[oi * NS + sl] = h ? mom_mean(r.mom[sl]) : __longlong_as_double(0x7FF8000000000000ll);
+            if (a.out_cov) a.out_cov[oi * NS + sl] = h ? mom_cov(r.mom[sl]) : __longlong_as_double(0x7FF8000000000000ll);
+          }
+          if constexpr (X) {
+#pragma unroll
+            for (int f = 0; f < 2; ++f)
+#pragma unroll
+              for (int l = 0; l < N; ++l) {
+                const bool h = f < QCfg<N>::maxf;
+                if (a.out_al_s1) a.out_al_s1[(oi * 2 + f) * N + l] = h ? r.al[f][l].s1 : ~0ull;
+                if (a.out_al_s2) a.out_al_s2[(oi * 2 + f) * N + l] = h ? r.al[f][l].s2 : ~0ull;
+              }
           }
           if (a.out_score) a.out_score[oi] = r.score;
           if (a.out_valid) a.out_valid[oi] = r.valid ? 1 : 0;
@@ -473,7 +535,7 @@ __global__ void __launch_bounds__(256) eval_kernel(EvalArgs a) {
               // `sl` is uniform: one scalar branch per slot keeps r.mom in
               // registers (a select chain here gets turned into scratch).
 #pragma unroll
-              for (int q = 0; q < NSLOT; ++q)
+              for (int q = 0; q < NS; ++q)
                 if ((uint32_t)q == sl) key[o] = kind == OBJ_MEAN ? r.mom[q].s1 : cov_key(r.mom[q]);
             }
           }
@@ -634,9 +696,9 @@ __global__ void __launch_bounds__(256) best_leader_kernel(SingleArgs a, const ui
 }
 
 // ------------------------------------------------------------- launchers --
-template <int N, bool FULL>
+template <int N, bool FULL, bool X>
 static hipError_t launch_eval_n(const EvalArgs& a, uint32_t grid, uint32_t bd, size_t shm, hipStream_t st) {
-  auto k = eval_kernel<N, FULL>;
+  auto k = eval_kernel<N, FULL, X>;
   hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k, dim3(grid), dim3(bd), shm, st, a);
@@ -646,21 +708,26 @@ static hipError_t launch_eval_n(const EvalArgs& a, uint32_t grid, uint32_t bd, s
 size_t eval_smem_bytes(const EvalArgs& a, uint32_t n, uint32_t bd, bool topk) {
   size_t off[11];
   int nl = 0;
+  const bool x = a.keys != 0;
   switch (n) {
-#define NL_CASE(NN) case NN: nl = QCfg<NN>::NL; break;
+#define NL_CASE(NN) case NN: nl = x ? QTab<NN, true>::NT : QTab<NN, false>::NT; break;
     NL_CASE(2) NL_CASE(3) NL_CASE(4) NL_CASE(5) NL_CASE(6) NL_CASE(7) NL_CASE(8) NL_CASE(9)
     NL_CASE(10) NL_CASE(11) NL_CASE(12) NL_CASE(13) NL_CASE(14) NL_CASE(15) NL_CASE(16)
 #undef NL_CASE
     default: return 0;
   }
-  return smem_layout(a, (int)n, nl <= 2 ? 1 : 2, bd, topk, off);
+  return smem_layout(a, (int)n, (nl + 1) / 2, bd, topk, off);
 }
 
-int eval_occupancy(uint32_t n, bool full, uint32_t bd, size_t shm) {
+int eval_occupancy(uint32_t n, bool full, uint32_t bd, size_t shm, bool x) {
   int nb = 0;
   const void* k = nullptr;
   switch (n) {
-#define OCC_CASE(NN) case NN: k = full ? (const void*)eval_kernel<NN, true> : (const void*)eval_kernel<NN, false>; break;
+#define OCC_CASE(NN)                                                                                       \
+  case NN:                                                                                                 \
+    k = x ? (full ? (const void*)eval_kernel<NN, true, true> : (const void*)eval_kernel<NN, false, true>)  \
+          : (full ? (const void*)eval_kernel<NN, true, false> : (const void*)eval_kernel<NN, false, false>); \
+    break;
     OCC_CASE(2) OCC_CASE(3) OCC_CASE(4) OCC_CASE(5) OCC_CASE(6) OCC_CASE(7) OCC_CASE(8) OCC_CASE(9)
     OCC_CASE(10) OCC_CASE(11) OCC_CASE(12) OCC_CASE(13) OCC_CASE(14) OCC_CASE(15) OCC_CASE(16)
 #undef OCC_CASE
@@ -674,8 +741,12 @@ int eval_occupancy(uint32_t n, bool full, uint32_t bd, size_t shm) {
 hipError_t launch_eval(const EvalArgs& a, uint32_t n, bool full, uint32_t grid, uint32_t bd, size_t shm,
                        hipStream_t st) {
   switch (n) {
-#define EV_CASE(NN) \
-  case NN: return full ? launch_eval_n<NN, true>(a, grid, bd, shm, st) : launch_eval_n<NN, false>(a, grid, bd, shm, st);
+#define EV_CASE(NN)                                                                                 \
+  case NN:                                                                                          \
+    return a.keys ? (full ? launch_eval_n<NN, true, true>(a, grid, bd, shm, st)                     \
+                          : launch_eval_n<NN, false, true>(a, grid, bd, shm, st))                   \
+                  : (full ? launch_eval_n<NN, true, false>(a, grid, bd, shm, st)                    \
+                          : launch_eval_n<NN, false, false>(a, grid, bd, shm, st));
     EV_CASE(2) EV_CASE(3) EV_CASE(4) EV_CASE(5) EV_CASE(6) EV_CASE(7) EV_CASE(8) EV_CASE(9)
     EV_CASE(10) EV_CASE(11) EV_CASE(12) EV_CASE(13) EV_CASE(14) EV_CASE(15) EV_CASE(16)
 #undef EV_CASE

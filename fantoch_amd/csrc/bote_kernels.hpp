@@ -33,7 +33,10 @@ struct EvalArgs {
   int want_score;
   double p_fmean, p_emean, p_fair;
   int ft_metric;
-  // FULL outputs
+  // key set: 0 compute_stats' 10 slots; 1 the extended key set (slots
+  // 10..19 and every leader's FPaxos moments; include/bote_hip.h)
+  uint32_t keys;
+  // FULL outputs (moments: NSLOT or, with keys, NSLOT_X per config)
   uint32_t* out_vals;
   uint32_t* out_leader;
   uint64_t* out_s1;
@@ -42,6 +45,8 @@ struct EvalArgs {
   double* out_cov;
   double* out_score;
   uint8_t* out_valid;
+  uint64_t* out_al_s1;  // keys: ncfg x 2 x n, all leaders (f = 1, 2; config order)
+  uint64_t* out_al_s2;
   // TOP-K outputs
   int n_obj;
   uint32_t obj_kind[MAXOBJ];
@@ -94,6 +99,7 @@ struct FastArgs {
   uint32_t gqsh;      // group kernel: log2 of the qtab plane stride in bytes (1 << gqsh >= gbd * 4)
   uint32_t gslots;    // group kernel, n <= 7: client lines per wave (0: none), see bote_group.hip
   uint32_t grx;       // group kernel, n <= 7: per-group position table (1) or per-lane row sorts (0)
+  uint32_t keys;      // group kernel: 1 = the extended key set (n = 4..7, default objectives first)
   // group kernel work distribution: nwchunks > 0: waves take cost-balanced
   // rank chunks [wchunks[c], wchunks[c+1]) from the ticket counter *wctr
   // (zeroed before each launch); 0: each wave sweeps an equal share of ranks
@@ -159,13 +165,14 @@ int fast_occupancy(uint32_t n, size_t shm);
 hipError_t launch_fast(const FastArgs& a, uint32_t n, uint32_t grid, size_t shm, hipStream_t st);
 size_t group_smem_bytes(const FastArgs& a, uint32_t n);
 bool group_uses_lines(uint32_t n);  // n <= 7: client lines (FastArgs::gslots) and register lookups
+bool group_supports_keys(uint32_t n, uint32_t bd);  // the extended key set on the group kernel (n = 4..7, bd <= 256)
 // workgroups per CU of the kernel instantiation launch_group runs for `a`
 // (workgroup size a.gbd)
 int group_occupancy(const FastArgs& a, uint32_t n, size_t shm, bool def_objectives);
 hipError_t launch_group(const FastArgs& a, uint32_t n, bool def_objectives, uint32_t grid, size_t shm, hipStream_t st);
 
 size_t eval_smem_bytes(const EvalArgs& a, uint32_t n, uint32_t bd, bool topk);
-int eval_occupancy(uint32_t n, bool full, uint32_t bd, size_t shm);
+int eval_occupancy(uint32_t n, bool full, uint32_t bd, size_t shm, bool keys = false);
 hipError_t launch_eval(const EvalArgs& a, uint32_t n, bool full, uint32_t grid, uint32_t bd, size_t shm,
                        hipStream_t st);
 hipError_t launch_merge(const Rec* src, uint32_t n_lists, uint64_t list_stride, Rec* dst, uint64_t out_stride,

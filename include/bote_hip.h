@@ -63,6 +63,28 @@ extern "C" {
 #define BOTE_SLOT_COLOCATED 5
 #define BOTE_NSLOTS 10
 
+/* Key sets.  BOTE_KEYS_TEMPO_ALL_LEADERS (BASELINE config 5: "Tempo f=1,2 +
+ * FPaxos all leaders") adds to the compute_stats keys, per config:
+ *   * Tempo's tiny fast quorum 2f and write quorum f + 1
+ *     (fantoch/src/config.rs:317-329) through Bote::leaderless, Input and
+ *     Colocated: slot = 10 + 4 * placement + {TT1, TT2, TW1, TW2} offsets
+ *     (Tempo's non-tiny fast quorum n/2 + f is the Atlas key af{f});
+ *   * FPaxos with EVERY leader (Bote::all_leaders_stats, lib.rs:129-150) over
+ *     the Input clients at q = f + 1, f = 1..max_f: the digest consumes every
+ *     leader's moments, and slots FL1/FL2 hold the histogram of the best
+ *     leader by Stats::Mean (Bote::best_leader, lib.rs:99-121, first minimum).
+ * Slots with f = 2 exist only when max_f(n) >= 2. */
+#define BOTE_KEYS_BASE 0
+#define BOTE_KEYS_TEMPO_ALL_LEADERS 1
+#define BOTE_SLOT_TT1 10 /* Tempo tiny, f = 1 (q = 2), Input; + 4 = Colocated */
+#define BOTE_SLOT_TT2 11 /* Tempo tiny, f = 2 (q = 4) */
+#define BOTE_SLOT_TW1 12 /* Tempo write, f = 1 (q = 2) */
+#define BOTE_SLOT_TW2 13 /* Tempo write, f = 2 (q = 3) */
+#define BOTE_SLOT_X_COLOCATED 4
+#define BOTE_SLOT_FL1 18 /* FPaxos, best leader by mean, f = 1, Input */
+#define BOTE_SLOT_FL2 19 /* FPaxos, best leader by mean, f = 2, Input */
+#define BOTE_NSLOTS_X 20
+
 /* Objectives of the streaming top-K (an extension: the reference stores every
  * config, search.rs:234-260; the MI355X build streams and keeps the best K). */
 #define BOTE_OBJ_SCORE 0 /* max Search::compute_score among valid configs (search.rs:421-472) */
@@ -174,6 +196,17 @@ int bote_eval(const bote_planet* p, const uint32_t* servers, uint32_t ns,
               uint32_t* out_vals, uint32_t* out_leader, uint64_t* out_sum, uint64_t* out_sumsq,
               double* out_mean, double* out_cov, double* out_score, uint8_t* out_valid);
 
+/* bote_eval with a key set: exact moments of every slot of `keys`
+ * (BOTE_KEYS_*), config-major: out_sum, out_sumsq ncfg x 20 (slots absent for
+ * n hold ~0; with BOTE_KEYS_BASE only the first 10 of each row are written,
+ * stride 10), out_leader as bote_eval, and with BOTE_KEYS_TEMPO_ALL_LEADERS
+ * every leader's FPaxos moments out_al_sum, out_al_sumsq ncfg x 2 x n
+ * (f = 1, 2; leaders in config order; ~0 when f > max_f(n)). */
+int bote_eval_keys(const bote_planet* p, const uint32_t* servers, uint32_t ns,
+                   const uint32_t* clients, uint32_t nc, uint32_t n, const uint32_t* configs,
+                   uint64_t rank_begin, uint64_t ncfg, uint32_t keys, uint32_t* out_leader,
+                   uint64_t* out_sum, uint64_t* out_sumsq, uint64_t* out_al_sum, uint64_t* out_al_sumsq);
+
 /* Bote::leaderless (lib.rs:38-59) for a batch of configurations (as in
  * bote_eval: `configs` or colex ranks) and nq quorum sizes (1..8, each <= n) at
  * once.  This carries Tempo (fantoch/src/config.rs:317-329): fast quorum
@@ -229,6 +262,17 @@ int bote_sweep_create_ex(const bote_planet* p, const uint32_t* servers, uint32_t
                          const uint32_t* clients, uint32_t nc, uint32_t n,
                          const bote_objective* objs, uint32_t n_obj, uint32_t K,
                          const bote_ranking_params* rp, int digest, int kernel, bote_sweep** out);
+/* bote_sweep_create_ex with a key set (BOTE_KEYS_*): objectives may name
+ * every slot of the set, and the digest folds all of its moments (DESIGN.md
+ * §7).  The extended set runs on the group kernel for n = 4..7 with config
+ * 5's objectives (SCORE, MEAN af1, MEAN ff1, COV af1, MEAN e, MEAN TT1, MEAN
+ * TW2, MEAN FL1, compiled in), otherwise on the generic kernel (any
+ * objectives). */
+int bote_sweep_create_keys(const bote_planet* p, const uint32_t* servers, uint32_t ns,
+                           const uint32_t* clients, uint32_t nc, uint32_t n,
+                           const bote_objective* objs, uint32_t n_obj, uint32_t K,
+                           const bote_ranking_params* rp, int digest, int kernel, uint32_t keys,
+                           bote_sweep** out);
 /* Asynchronous on `hip_stream`: the sweep kernel, the exact fix-up of its
  * deferred near-tie configs, the (device-decided) overflow fallback and the
  * merge chain are all stream-ordered; no host synchronisation. */
@@ -291,12 +335,13 @@ int bote_sweep_destroy(bote_sweep* s);
  * device, and a (key, rank) merge tree there.  It may be called repeatedly
  * (each launch recomputes the whole range).  bote_search_result waits for the
  * last launch and copies out as bote_sweep_result; the result equals one
- * unsharded sweep.  Calls on one handle must not overlap. */
+ * unsharded sweep.  `keys` selects the key set (BOTE_KEYS_*, as
+ * bote_sweep_create_keys).  Calls on one handle must not overlap. */
 int bote_search_create(const bote_planet* const* planets, uint32_t n_devices,
                        const uint32_t* servers, uint32_t ns, const uint32_t* clients, uint32_t nc,
                        uint32_t n, uint64_t rank_begin, uint64_t rank_end,
                        const bote_objective* objs, uint32_t n_obj, uint32_t K,
-                       const bote_ranking_params* rp, int digest, bote_search** out);
+                       const bote_ranking_params* rp, int digest, uint32_t keys, bote_search** out);
 int bote_search_launch(bote_search* h);
 int bote_search_result(bote_search* h, bote_topk_record* out, uint32_t* out_count,
                        uint64_t* out_valid, uint64_t* out_digest);

@@ -23,6 +23,9 @@
 //    * FTMetric::fs, max_f                               fantoch_bote/src/search.rs:474-477,652-666
 //    * Tempo quorum sizes (fast n/2+f, tiny 2f, write f+1) fantoch/src/config.rs:317-329 (through
 //      Bote::leaderless, oracle_leaderless_batch)
+//    * the extended key set (BOTE_KEYS_TEMPO_ALL_LEADERS, BASELINE config 5):
+//      Tempo tiny/write leaderless keys and FPaxos all_leaders_stats per
+//      config (compute_stats_x), as the GPU sweep computes them
 //
 //  Pinned against the reference's own known-answer tests (tests/test_oracle.py):
 //  lib.rs:193-465, protocol.rs:118-154, search.rs:671-751, histogram.rs:390-463,
@@ -253,6 +256,13 @@ size_t max_f(size_t n) { return std::min(n / 2, (size_t)2); }
 // Key slots shared with the GPU path: slot = base + 5 * placement,
 // base: 0 af1, 1 ff1, 2 af2, 3 ff2, 4 e; placement 0 Input, 1 Colocated.
 enum { K_AF1 = 0, K_FF1 = 1, K_AF2 = 2, K_FF2 = 3, K_E = 4, NKEYS = 10 };
+// Extended key set (an extension of compute_stats for BASELINE config 5;
+// include/bote_hip.h): Tempo tiny fast (q = 2f) and write (q = f + 1)
+// leaderless keys, slot 10 + 4 * placement + {tt1, tt2, tw1, tw2}; FPaxos
+// under the best-by-MEAN leader (best_leader with Stats::Mean), Input, slots
+// 18 (f = 1) and 19 (f = 2); plus every leader's FPaxos histogram (Input,
+// f = 1..max_f), which only feeds the digest.
+enum { K_TT1 = 10, K_TT2 = 11, K_TW1 = 12, K_TW2 = 13, K_FL1 = 18, K_FL2 = 19, NKEYS_X = 20 };
 int slot_atlas(size_t f) { return f == 1 ? K_AF1 : K_AF2; }
 int slot_fpaxos(size_t f) { return f == 1 ? K_FF1 : K_FF2; }
 
@@ -331,11 +341,13 @@ struct Bote {
 
 // ------------------------------------------------------------ Stats (10) ----
 struct ProtocolStats {
-  bool has[NKEYS] = {};
-  Histogram h[NKEYS];
-  std::vector<uint64_t> raw[NKEYS];  // per-client values, client order
-  uint32_t leader = 0;               // region id of the FPaxos leader
-  size_t leader_pos = 0;             // index of the leader inside `config`
+  bool has[NKEYS_X] = {};
+  Histogram h[NKEYS_X];
+  std::vector<uint64_t> raw[NKEYS_X];  // per-client values, client order
+  uint32_t leader = 0;                 // region id of the FPaxos leader
+  size_t leader_pos = 0;               // index of the leader inside `config`
+  // extended key set: all_leaders_stats per f = 1..max_f, leaders in config order
+  std::vector<Histogram> all_leaders[2];
 };
 
 // search.rs:262-319
@@ -366,6 +378,43 @@ void compute_stats(const Bote& bote, const std::vector<uint32_t>& config,
     st.h[se] = Histogram::from(e.begin(), e.end());
     st.raw[se] = std::move(e);
     st.has[se] = true;
+  }
+}
+
+// The extended key set (BASELINE config 5: "Tempo f=1,2 + FPaxos all
+// leaders"): compute_stats plus, per placement and f = 1..max_f, Tempo's
+// tiny fast quorum 2f and write quorum f + 1 through Bote::leaderless
+// (fantoch/src/config.rs:317-329; the non-tiny fast quorum n/2 + f is the
+// Atlas key already), and over the Input clients all_leaders_stats at
+// q = f + 1 (lib.rs:129-150) with its best leader by Stats::Mean (lib.rs:99-121).
+void compute_stats_x(const Bote& bote, const std::vector<uint32_t>& config,
+                     const std::vector<uint32_t>& all_clients, ProtocolStats& st) {
+  compute_stats(bote, config, all_clients, st);
+  const size_t n = config.size();
+  for (int p = 0; p < 2; ++p) {
+    const std::vector<uint32_t>& clients = p == 0 ? all_clients : config;
+    for (size_t f = 1; f <= max_f(n); ++f) {
+      const int tt = K_TT1 + (int)(f - 1) + 4 * p, tw = K_TW1 + (int)(f - 1) + 4 * p;
+      auto a = bote.leaderless(config, clients, 2 * f);
+      st.h[tt] = Histogram::from(a.begin(), a.end());
+      st.raw[tt] = std::move(a);
+      st.has[tt] = true;
+      auto w = bote.leaderless(config, clients, f + 1);
+      st.h[tw] = Histogram::from(w.begin(), w.end());
+      st.raw[tw] = std::move(w);
+      st.has[tw] = true;
+    }
+  }
+  for (size_t f = 1; f <= max_f(n); ++f) {
+    auto al = bote.all_leaders_stats(config, all_clients, quorum_size(FPAXOS, n, f));
+    st.all_leaders[f - 1].clear();
+    for (auto& e : al) st.all_leaders[f - 1].push_back(e.second);
+    Histogram best;
+    const size_t b = bote.best_leader(config, all_clients, quorum_size(FPAXOS, n, f), 0, &best);
+    (void)b;
+    const int fl = K_FL1 + (int)(f - 1);
+    st.h[fl] = best;
+    st.has[fl] = true;
   }
 }
 
@@ -507,17 +556,33 @@ uint64_t mix64(uint64_t z) {
 // Order-independent per-config digest shared with the GPU path (DESIGN.md
 // "Digest"): a 32-bit fold of every present slot's exact sum and sum of
 // squares, then one mix64 with the rank and the leader position.
+// With the extended key set (compute_stats_x) a second term is added: hx
+// folds, from 0, every leader's FPaxos histogram (f = 1, then f = 2; leaders
+// in config order), then the present slots 18, 19, 14, 15, 16, 17, 10, 11,
+// 12, 13; the term is mix64(~rank ^ (hx << 24)).
 uint64_t config_digest(uint64_t rank, const ProtocolStats& st) {
-  uint32_t h = 0;
-  for (int s = 0; s < NKEYS; ++s) {
-    if (!st.has[s]) continue;
+  auto fold = [](uint32_t h, const Histogram& hh) {
     uint64_t s1, c;
-    st.h[s].sum_and_count(s1, c);
-    uint64_t s2 = st.h[s].sumsq();
+    hh.sum_and_count(s1, c);
+    uint64_t s2 = hh.sumsq();
     h = (h ^ (uint32_t)s1) * 0x9E3779B1u;
     h = (h ^ (uint32_t)(s2 ^ (s2 >> 32))) * 0x85EBCA77u;
+    return h;
+  };
+  uint32_t h = 0;
+  for (int s = 0; s < NKEYS; ++s)
+    if (st.has[s]) h = fold(h, st.h[s]);
+  uint64_t d = mix64(rank ^ ((uint64_t)st.leader_pos << 56) ^ ((uint64_t)h << 24));
+  if (!st.all_leaders[0].empty()) {  // the extended key set
+    uint32_t hx = 0;
+    for (int f = 0; f < 2; ++f)
+      for (auto& hh : st.all_leaders[f]) hx = fold(hx, hh);
+    static const int order[10] = {18, 19, 14, 15, 16, 17, 10, 11, 12, 13};
+    for (int s : order)
+      if (st.has[s]) hx = fold(hx, st.h[s]);
+    d += mix64(~rank ^ ((uint64_t)hx << 24));
   }
-  return mix64(rank ^ ((uint64_t)st.leader_pos << 56) ^ ((uint64_t)h << 24));
+  return d;
 }
 
 thread_local std::string g_err;
@@ -752,11 +817,12 @@ void oracle_colex_unrank(uint64_t rank, uint32_t n, uint32_t ns, uint32_t* out) 
 //   out_valid:  number of configs with a valid compute_score
 //   out_digest: wrapping sum of per-config digests
 //   threads:    std::thread workers over contiguous rank chunks
-int oracle_sweep(void* h, const uint32_t* servers, uint32_t ns, const uint32_t* clients,
-                 uint32_t nc, uint32_t n, uint64_t rb, uint64_t re, const uint32_t* objs,
-                 uint32_t n_obj, uint32_t K, const double* rparams, int ft_metric,
-                 uint32_t threads, uint64_t* out_key, uint64_t* out_rank, uint32_t* out_cnt,
-                 uint64_t* out_valid, uint64_t* out_digest) {
+//   keys:       0 the compute_stats keys; 1 the extended key set (compute_stats_x)
+int oracle_sweep_x(void* h, const uint32_t* servers, uint32_t ns, const uint32_t* clients,
+                   uint32_t nc, uint32_t n, uint64_t rb, uint64_t re, const uint32_t* objs,
+                   uint32_t n_obj, uint32_t K, const double* rparams, int ft_metric, uint32_t keys,
+                   uint32_t threads, uint64_t* out_key, uint64_t* out_rank, uint32_t* out_cnt,
+                   uint64_t* out_valid, uint64_t* out_digest) {
   ORACLE_TRY
   const Planet* P = (Planet*)h;
   Bote b{P};
@@ -778,7 +844,8 @@ int oracle_sweep(void* h, const uint32_t* servers, uint32_t ns, const uint32_t* 
         colex_unrank(B, r, n, ns, pos.data());
         for (uint32_t j = 0; j < n; ++j) cfg[j] = servers[pos[j]];
         ProtocolStats st;
-        compute_stats(b, cfg, cl, st);
+        if (keys) compute_stats_x(b, cfg, cl, st);
+        else compute_stats(b, cfg, cl, st);
         double score;
         if (compute_score(n, st, rp, score)) valid[t]++;
         digest[t] += config_digest(r, st);
@@ -813,6 +880,68 @@ int oracle_sweep(void* h, const uint32_t* servers, uint32_t ns, const uint32_t* 
       out_rank[(size_t)o * K + i] = m.v[i].second;
     }
   }
+  ORACLE_CATCH
+}
+
+int oracle_sweep(void* h, const uint32_t* servers, uint32_t ns, const uint32_t* clients,
+                 uint32_t nc, uint32_t n, uint64_t rb, uint64_t re, const uint32_t* objs,
+                 uint32_t n_obj, uint32_t K, const double* rparams, int ft_metric,
+                 uint32_t threads, uint64_t* out_key, uint64_t* out_rank, uint32_t* out_cnt,
+                 uint64_t* out_valid, uint64_t* out_digest) {
+  return oracle_sweep_x(h, servers, ns, clients, nc, n, rb, re, objs, n_obj, K, rparams, ft_metric, 0, threads,
+                        out_key, out_rank, out_cnt, out_valid, out_digest);
+}
+
+// compute_stats_x (the extended key set) for a batch of explicit configs
+// (region ids, config order): exact moments per slot and per leader.
+//   out_s1, out_s2:   ncfg x 20 (slots 0..19; ~0 where a slot is absent)
+//   out_al1, out_al2: ncfg x 2 x n (all leaders, f = 1, 2, config order; ~0 when f > max_f)
+//   out_leader:       ncfg COV-best leader positions (compute_stats)
+int oracle_moments_x(void* h, const uint32_t* configs, uint32_t ncfg, uint32_t n, const uint32_t* clients,
+                     uint32_t nc, uint32_t threads, uint64_t* out_s1, uint64_t* out_s2, uint64_t* out_al1,
+                     uint64_t* out_al2, uint32_t* out_leader) {
+  ORACLE_TRY
+  Bote b{(Planet*)h};
+  std::vector<uint32_t> cl(clients, clients + nc);
+  if (threads == 0) threads = 1;
+  std::vector<std::string> errs(threads);
+  auto work = [&](uint32_t t) {
+    try {
+      for (uint64_t i = (uint64_t)ncfg * t / threads; i < (uint64_t)ncfg * (t + 1) / threads; ++i) {
+        std::vector<uint32_t> cfg(configs + i * n, configs + (i + 1) * n);
+        ProtocolStats st;
+        compute_stats_x(b, cfg, cl, st);
+        for (int s = 0; s < NKEYS_X; ++s) {
+          uint64_t s1 = ~0ull, c = 0, s2 = ~0ull;
+          if (st.has[s]) {
+            st.h[s].sum_and_count(s1, c);
+            s2 = st.h[s].sumsq();
+          }
+          out_s1[i * NKEYS_X + s] = s1;
+          out_s2[i * NKEYS_X + s] = s2;
+        }
+        for (int f = 0; f < 2; ++f)
+          for (uint32_t l = 0; l < n; ++l) {
+            uint64_t s1 = ~0ull, c = 0, s2 = ~0ull;
+            if (l < st.all_leaders[f].size()) {
+              st.all_leaders[f][l].sum_and_count(s1, c);
+              s2 = st.all_leaders[f][l].sumsq();
+            }
+            out_al1[(i * 2 + f) * n + l] = s1;
+            out_al2[(i * 2 + f) * n + l] = s2;
+          }
+        out_leader[i] = (uint32_t)st.leader_pos;
+      }
+    } catch (const std::exception& ex) {
+      errs[t] = ex.what();
+    }
+  };
+  std::vector<std::thread> pool;
+  for (uint32_t t = 1; t < threads; ++t) pool.emplace_back(work, t);
+  work(0);
+  for (auto& th : pool) th.join();
+  for (auto& e : errs)
+    if (!e.empty()) throw Panic(e);
   ORACLE_CATCH
 }
 

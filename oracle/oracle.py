@@ -70,6 +70,11 @@ def lib():
         L.oracle_scores.argtypes = [C.c_void_p, u32p, C.c_uint32, C.c_uint32, u32p, C.c_uint32, f64p, C.c_int,
                                     f64p, np.ctypeslib.ndpointer(np.uint8, flags="C_CONTIGUOUS")]
         L.oracle_colex_unrank.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32, u32p]
+        L.oracle_sweep_x.argtypes = [C.c_void_p, u32p, C.c_uint32, u32p, C.c_uint32, C.c_uint32, C.c_uint64,
+                                     C.c_uint64, u32p, C.c_uint32, C.c_uint32, f64p, C.c_int, C.c_uint32,
+                                     C.c_uint32, u64p, u64p, u32p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
+        L.oracle_moments_x.argtypes = [C.c_void_p, u32p, C.c_uint32, C.c_uint32, u32p, C.c_uint32, C.c_uint32,
+                                       u64p, u64p, u64p, u64p, u32p]
         L.oracle_sweep.argtypes = [C.c_void_p, u32p, C.c_uint32, u32p, C.c_uint32, C.c_uint32,
                                    C.c_uint64, C.c_uint64, u32p, C.c_uint32, C.c_uint32, f64p, C.c_int,
                                    C.c_uint32, u64p, u64p, u32p, C.POINTER(C.c_uint64),
@@ -175,20 +180,36 @@ class OraclePlanet:
                                    np.asarray(rparams, dtype=np.float64), ft_metric, sc, va))
         return sc, va
 
+    def moments_x(self, configs: np.ndarray, clients, threads: int = 1):
+        """compute_stats_x (the extended key set) per config: (s1, s2) of shape
+        (ncfg, 20), all-leader (s1, s2) of shape (ncfg, 2, n), COV leaders."""
+        cfg = np.ascontiguousarray(np.asarray(configs, dtype=np.uint32))
+        ncfg, n = cfg.shape
+        c = _u32(clients)
+        s1 = np.zeros((ncfg, 20), np.uint64)
+        s2 = np.zeros((ncfg, 20), np.uint64)
+        a1 = np.zeros((ncfg, 2, n), np.uint64)
+        a2 = np.zeros((ncfg, 2, n), np.uint64)
+        lead = np.zeros(ncfg, np.uint32)
+        _check(lib().oracle_moments_x(self.h, cfg.reshape(-1), ncfg, n, c, len(c), threads, s1.reshape(-1),
+                                      s2.reshape(-1), a1.reshape(-1), a2.reshape(-1), lead))
+        return s1, s2, a1, a2, lead
+
     def sweep(self, servers, clients, n: int, rb: int, re: int, objectives, K: int,
-              rparams=(110.0, 35.0, 0.0, 15.0), ft_metric: int = 2, threads: int = 1):
+              rparams=(110.0, 35.0, 0.0, 15.0), ft_metric: int = 2, threads: int = 1, keys: int = 0):
+        """Streaming sweep; keys=1 computes the extended key set (compute_stats_x)."""
         s, c = _u32(servers), _u32(clients)
         objs = _u32(np.asarray(objectives, dtype=np.uint32).reshape(-1))
         nobj = len(objs) // 2
-        keys = np.zeros(nobj * K, np.uint64)
+        kv = np.zeros(nobj * K, np.uint64)
         ranks = np.zeros(nobj * K, np.uint64)
         cnt = np.zeros(nobj, np.uint32)
         valid, digest = C.c_uint64(), C.c_uint64()
         rp = np.asarray(rparams, dtype=np.float64)
-        _check(lib().oracle_sweep(self.h, s, len(s), c, len(c), n, rb, re, objs, nobj, K, rp,
-                                  ft_metric, threads, keys, ranks, cnt, C.byref(valid),
-                                  C.byref(digest)))
-        tops = [list(zip(keys[o * K:o * K + cnt[o]].tolist(), ranks[o * K:o * K + cnt[o]].tolist()))
+        _check(lib().oracle_sweep_x(self.h, s, len(s), c, len(c), n, rb, re, objs, nobj, K, rp,
+                                    ft_metric, keys, threads, kv, ranks, cnt, C.byref(valid),
+                                    C.byref(digest)))
+        tops = [list(zip(kv[o * K:o * K + cnt[o]].tolist(), ranks[o * K:o * K + cnt[o]].tolist()))
                 for o in range(nobj)]
         return tops, valid.value, digest.value
 

@@ -36,8 +36,9 @@ def merge_blocks(blocks, n_obj):
 
 
 class OracleSweep:
-    def __init__(self, oplanet, servers, clients, n, objectives, K, rparams=(110.0, 35.0, 0.0, 15.0)):
-        self.o, self.n, self.K = oplanet, n, K
+    def __init__(self, oplanet, servers, clients, n, objectives, K, rparams=(110.0, 35.0, 0.0, 15.0), keys=0,
+                 threads=2):
+        self.o, self.n, self.K, self.keys, self.threads = oplanet, n, K, keys, threads
         self.servers = np.asarray(servers, dtype=np.uint32)
         self.clients = np.asarray(clients, dtype=np.uint32)
         self.objectives = list(objectives)
@@ -47,7 +48,7 @@ class OracleSweep:
 
     def launch(self, rb, re, stream=None):
         tops, valid, digest = self.o.sweep(self.servers, self.clients, self.n, rb, re, self.objectives, self.K,
-                                           self.rparams, 2, 2)
+                                           self.rparams, 2, self.threads, keys=self.keys)
         no = len(self.objectives)
         blk = np.full(no * KP * 2 + 2, PAD, dtype=np.uint64)
         for o, lst in enumerate(tops):

@@ -1,0 +1,157 @@
+"""GPU parity of the extended key set (BASELINE config 5: "Tempo f=1,2 +
+FPaxos all leaders"; include/bote_hip.h BOTE_KEYS_TEMPO_ALL_LEADERS) against
+the CPU oracle (compute_stats_x: Tempo tiny/write keys through
+Bote::leaderless, lib.rs:38-59 / config.rs:317-329; FPaxos all_leaders_stats,
+lib.rs:129-150, best leader by Stats::Mean, lib.rs:99-121):
+  * exact moments of all 20 slots and every leader's FPaxos moments per
+    config (bote_eval_keys) on GCP n = 2..13 and the synthetic R=64 / R=128
+    planets, at random ranks and in unsorted config orders;
+  * the streaming sweep with the extended keys (group kernel for n = 4..7,
+    generic otherwise, and both forced) against tests/golden/topk_x.json:
+    every GCP config of n = 2..13 and synthetic sub-ranges;
+  * BASELINE config 5 at full size through the seeded random R=128 n=6
+    windows of tests/golden/syn_r128n6_windows.json, and the whole rank space
+    on the group kernel equal to the generic kernel."""
+import json
+import os
+from math import comb
+
+import numpy as np
+import pytest
+
+import oracle as O
+from fantoch_amd import _lib
+from fantoch_amd.bote import (CONFIG5_OBJECTIVES, DEFAULT_RANKING, DevicePlanet, MultiDeviceSearch, Sweep,
+                              eval_keys)
+from fantoch_amd.planet import Planet
+
+pytestmark = pytest.mark.gpu
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+U64MAX = np.iinfo(np.uint64).max
+
+
+def _fixture(name):
+    path = os.path.join(GOLDEN, name)
+    if not os.path.exists(path):
+        pytest.skip(f"{name} not generated yet (tests/golden/make_keys_golden.py)")
+    return json.load(open(path))
+
+
+def _planet(kind):
+    return Planet.new() if kind == "gcp" else Planet.synthetic(int(kind[3:]))
+
+
+@pytest.mark.parametrize("kind,n", [("gcp", n) for n in range(2, 14)] + [("syn64", 7), ("syn128", 6), ("syn64", 4)])
+def test_eval_keys_vs_oracle(kind, n):
+    p = _planet(kind)
+    dp, o = DevicePlanet(p), O.OraclePlanet.of(p)
+    srv = np.arange(p.R, dtype=np.uint32)
+    rng = np.random.default_rng(100 + n)
+    total = comb(p.R, n)
+    ranks = np.unique(rng.integers(0, total, size=min(total, 1500)))
+    cfg = np.array([_lib.colex_unrank(int(r), n, p.R) for r in ranks], dtype=np.uint32)
+    # half of them in a shuffled config order (leader ties, all-leader order)
+    for i in range(0, len(cfg), 2):
+        cfg[i] = rng.permutation(cfg[i])
+    got = eval_keys(dp, srv, srv, n, configs=cfg)
+    s1, s2, a1, a2, lead = o.moments_x(cfg, srv, threads=8)
+    assert np.array_equal(got.leader, lead)
+    assert np.array_equal(got.s1, s1) and np.array_equal(got.s2, s2)
+    if min(n // 2, 2) < 2:  # f = 2 leaders do not exist
+        a1[:, 1, :] = U64MAX
+        a2[:, 1, :] = U64MAX
+    assert np.array_equal(got.al_s1, a1) and np.array_equal(got.al_s2, a2)
+    # contiguous colex ranks too (no explicit configs)
+    rb = int(rng.integers(0, max(1, total - 300)))
+    cnt = min(300, total - rb)
+    got = eval_keys(dp, srv, srv, n, rank_begin=rb, ncfg=cnt)
+    cfg = np.array([_lib.colex_unrank(r, n, p.R) for r in range(rb, rb + cnt)], dtype=np.uint32)
+    s1, s2, a1, a2, lead = o.moments_x(cfg, srv, threads=8)
+    assert np.array_equal(got.s1, s1) and np.array_equal(got.leader, lead)
+
+
+def _cases():
+    path = os.path.join(GOLDEN, "topk_x.json")
+    return list(json.load(open(path))["cases"]) if os.path.exists(path) else []
+
+
+@pytest.mark.parametrize("case", _cases())
+def test_sweep_keys_vs_fixture(case):
+    t = _fixture("topk_x.json")
+    c = t["cases"][case]
+    p = _planet("gcp" if case.startswith("gcp") else f"syn{c['R']}")
+    dp = DevicePlanet(p)
+    s = np.arange(p.R, dtype=np.uint32)
+    objs = [tuple(x) for x in c["objectives"]]
+    want = (c["valid"], c["digest"], c["tops"])
+    kernels = [None, "generic"] + (["group"] if 4 <= c["n"] <= 7 else [])
+    for k in kernels:
+        sw = Sweep(dp, s, s, c["n"], objs, K=t["K"], ranking=DEFAULT_RANKING, digest=True, kernel=k,
+                   keys=_lib.KEYS_TEMPO_ALL_LEADERS)
+        if k is None and 4 <= c["n"] <= 7 and c["R"] >= 64:
+            assert sw.kernel_path() == "group"
+        sw.launch(c["rank_begin"], c["rank_end"])
+        r = sw.result()
+        got = (r.valid, str(r.digest), [[[str(kk), rr] for kk, rr in lst] for lst in r.tops])
+        assert got == want, f"kernel {k or 'auto'} ({sw.kernel_path()})"
+
+
+def test_r128n6_random_windows_keys_vs_oracle():
+    """BASELINE config 5 as stated (R=128 n=6, Tempo f=1,2 + FPaxos all leaders):
+    the 64 seeded random 10^5-rank windows with the extended key set, on the
+    group kernel, and two of them through a 2-shard bote_search handle."""
+    fx = _fixture("syn_r128n6_windows.json")
+    ws = [w for w in fx["windows"] if w.get("random") and "x" in w]
+    assert len(ws) >= 64
+    p = Planet.synthetic(128)
+    dp = DevicePlanet(p)
+    srv = np.arange(128, dtype=np.uint32)
+    objs = [tuple(o) for o in ws[0]["x"]["objectives"]]
+    assert objs == list(CONFIG5_OBJECTIVES)
+    sw = Sweep(dp, srv, srv, 6, objs, K=100, ranking=DEFAULT_RANKING, digest=True, keys=_lib.KEYS_TEMPO_ALL_LEADERS)
+    assert sw.kernel_path() == "group"
+    for w in ws:
+        sw.launch(w["rank_begin"], w["rank_end"])
+        r = sw.result()
+        x = w["x"]
+        assert (r.valid, r.digest) == (w["valid"], int(x["digest"])), w["rank_begin"]
+        assert [[(int(k), int(rk)) for k, rk in lst] for lst in r.tops] == \
+               [[(int(k), int(rk)) for k, rk in lst] for lst in x["tops"]], w["rank_begin"]
+    for w in ws[:2]:
+        h = MultiDeviceSearch([dp, dp], srv, srv, 6, objectives=objs, rank_begin=w["rank_begin"],
+                              rank_end=w["rank_end"], keys=_lib.KEYS_TEMPO_ALL_LEADERS)
+        h.launch()
+        r = h.result()
+        assert (r.valid, r.digest) == (w["valid"], int(w["x"]["digest"]))
+
+
+def test_r128n6_full_keys_group_equals_generic_on_a_slice():
+    """A 2*10^8-rank slice of config 5 with the extended key set: the group
+    kernel equals the exact generic kernel (every slot's and every leader's
+    moments through the digest, valid count, top-K)."""
+    p = Planet.synthetic(128)
+    dp = DevicePlanet(p)
+    srv = np.arange(128, dtype=np.uint32)
+    rb, re = 1_700_000_000, 1_900_000_000
+    out = {}
+    for k in ("group", "generic"):
+        sw = Sweep(dp, srv, srv, 6, CONFIG5_OBJECTIVES, K=100, ranking=DEFAULT_RANKING, digest=True, kernel=k,
+                   keys=_lib.KEYS_TEMPO_ALL_LEADERS)
+        sw.launch(rb, re)
+        r = sw.result()
+        out[k] = (r.valid, r.digest, r.tops)
+    assert out["group"] == out["generic"]
+
+
+def test_keys_argument_errors():
+    p = Planet.new()
+    dp = DevicePlanet(p)
+    s = np.arange(p.R, dtype=np.uint32)
+    with pytest.raises(_lib.BoteError, match="key set"):
+        Sweep(dp, s, s, 5, CONFIG5_OBJECTIVES, keys=7)
+    with pytest.raises(_lib.BoteError, match="slot"):  # extended slots need the extended key set
+        Sweep(dp, s, s, 5, CONFIG5_OBJECTIVES)
+    with pytest.raises(_lib.BoteError, match="max_f"):  # tw2 (f = 2) does not exist at n = 3
+        Sweep(dp, s, s, 3, CONFIG5_OBJECTIVES, keys=1)
+    with pytest.raises(_lib.BoteError, match="group kernel"):  # the group kernel needs the default objectives first
+        Sweep(dp, s, s, 5, [(_lib.OBJ_MEAN, _lib.SLOT_TT1)], keys=1, kernel="group")

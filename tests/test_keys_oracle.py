@@ -1,0 +1,69 @@
+"""The extended key set in the CPU oracle (compute_stats_x, BASELINE config 5:
+"Tempo f=1,2 + FPaxos all leaders"), against the oracle's reference-pinned
+single calls: Tempo's tiny (2f) and write (f + 1) keys are Bote::leaderless
+(lib.rs:38-59) at those quorum sizes (config.rs:317-329); the all-leader
+moments are Bote::leader per leader (lib.rs:67-89, all_leaders_stats
+lib.rs:129-150); fl1/fl2 are best_leader by Stats::Mean (lib.rs:99-121).
+CPU only."""
+import numpy as np
+import pytest
+
+import oracle as O
+from fantoch_amd import _lib
+from fantoch_amd.planet import Planet
+
+
+def _mom(v):
+    v = np.asarray(v, dtype=np.uint64)
+    return int(v.sum()), int((v * v).sum())
+
+
+@pytest.mark.parametrize("planet,n", [("gcp", 2), ("gcp", 3), ("gcp", 5), ("gcp", 7), ("gcp", 8), ("gcp", 13),
+                                      ("syn64", 7), ("syn128", 6)])
+def test_moments_x_equal_single_calls(planet, n):
+    p = Planet.new() if planet == "gcp" else Planet.synthetic(64 if planet == "syn64" else 128)
+    o = O.OraclePlanet.of(p)
+    rng = np.random.default_rng(n)
+    cfgs = np.array([rng.choice(p.R, n, replace=False) for _ in range(12)], dtype=np.uint32)
+    cli = np.arange(p.R, dtype=np.uint32)
+    s1, s2, a1, a2, lead = o.moments_x(cfgs, cli, threads=2)
+    mf = min(n // 2, 2)
+    vals, lead0 = o.compute_stats(cfgs, cli)
+    nc = len(cli)
+    for i, cfg in enumerate(cfgs):
+        assert lead[i] == lead0[i]
+        # the compute_stats slots are unchanged
+        for s in range(10):
+            seg = vals[i, s * nc:(s + 1) * nc] if s < 5 else vals[i, 5 * nc + (s - 5) * n:5 * nc + (s - 4) * n]
+            if seg[0] == np.iinfo(np.uint64).max:
+                assert s1[i, s] == np.iinfo(np.uint64).max
+            else:
+                assert (int(s1[i, s]), int(s2[i, s])) == _mom(seg)
+        for f in range(1, 3):
+            for pl, cl in ((0, cli), (1, cfg)):
+                tt, tw = _lib.SLOT_TT1 + f - 1 + 4 * pl, _lib.SLOT_TW1 + f - 1 + 4 * pl
+                if f > mf:
+                    assert s1[i, tt] == s1[i, tw] == np.iinfo(np.uint64).max
+                    continue
+                assert (int(s1[i, tt]), int(s2[i, tt])) == _mom(o.leaderless(cfg, cl, 2 * f))
+                assert (int(s1[i, tw]), int(s2[i, tw])) == _mom(o.leaderless(cfg, cl, f + 1))
+            if f > mf:
+                assert s1[i, _lib.SLOT_FL1 + f - 1] == np.iinfo(np.uint64).max
+                continue
+            per = [_mom(o.leader(int(l), cfg, cli, f + 1)) for l in cfg]
+            assert [(int(a1[i, f - 1, k]), int(a2[i, f - 1, k])) for k in range(n)] == per
+            best = o.best_leader(cfg, cli, f + 1, 0)  # Stats::Mean, first minimum
+            assert (int(s1[i, _lib.SLOT_FL1 + f - 1]), int(s2[i, _lib.SLOT_FL1 + f - 1])) == per[best]
+
+
+def test_sweep_x_keeps_base_results_and_changes_digest():
+    """The extended key set leaves valid counts and the compute_stats objectives
+    unchanged; its digest adds the second term."""
+    p = Planet.new()
+    o = O.OraclePlanet.of(p)
+    s = np.arange(p.R, dtype=np.uint32)
+    objs = [(0, 0), (1, 0), (1, 1), (2, 0), (1, 4)]
+    t0, v0, d0 = o.sweep(s, s, 5, 0, 15504, objs, 16, threads=4)
+    t1, v1, d1 = o.sweep(s, s, 5, 0, 15504, objs + [(1, 10), (1, 13), (1, 18)], 16, threads=4, keys=1)
+    assert v0 == v1 and t1[:5] == t0 and d0 != d1
+    assert all(len(t) == 16 for t in t1)
