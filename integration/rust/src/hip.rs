@@ -104,6 +104,23 @@ extern "C" {
                             objs: *const bote_objective, n_obj: u32, k: u32, rp: *const bote_ranking_params,
                             digest: c_int, out: *mut bote_topk_record, out_count: *mut u32, out_valid: *mut u64,
                             out_digest: *mut u64) -> c_int;
+    pub fn bote_search_create(planets: *const *const bote_planet, n_devices: u32, servers: *const u32, ns: u32,
+                              clients: *const u32, nc: u32, n: u32, rank_begin: u64, rank_end: u64,
+                              objs: *const bote_objective, n_obj: u32, k: u32, rp: *const bote_ranking_params,
+                              digest: c_int, keys: u32, out: *mut *mut bote_search) -> c_int;
+    pub fn bote_search_launch(h: *mut bote_search) -> c_int;
+    pub fn bote_search_result(h: *mut bote_search, out: *mut bote_topk_record, out_count: *mut u32,
+                              out_valid: *mut u64, out_digest: *mut u64) -> c_int;
+    pub fn bote_search_bounds(h: *const bote_search, out_bounds: *mut u64) -> c_int;
+    pub fn bote_search_destroy(h: *mut bote_search) -> c_int;
+    pub fn bote_sweep_create_keys(p: *const bote_planet, servers: *const u32, ns: u32, clients: *const u32, nc: u32,
+                                  n: u32, objs: *const bote_objective, n_obj: u32, k: u32,
+                                  rp: *const bote_ranking_params, digest: c_int, kernel: c_int, keys: u32,
+                                  out: *mut *mut bote_sweep) -> c_int;
+    pub fn bote_eval_keys(p: *const bote_planet, servers: *const u32, ns: u32, clients: *const u32, nc: u32,
+                          n: u32, configs: *const u32, rank_begin: u64, ncfg: u64, keys: u32, out_leader: *mut u32,
+                          out_sum: *mut u64, out_sumsq: *mut u64, out_al_sum: *mut u64, out_al_sumsq: *mut u64)
+        -> c_int;
     pub fn bote_evolving_chains(device: c_int, ns: u32, counts: *const u32, masks: *const *const u64,
                                 scores: *const *const f64, means: *const *const f64, min_mean_decrease: f64,
                                 ft_metric: c_int, max_out: u64, out_idx: *mut u32, out_score: *mut f64,

@@ -108,27 +108,67 @@ impl HipBote {
         stats
     }
 
-    /// The multi-GPU exhaustive search in one call (bote_search_topk): colex
-    /// ranks of n-subsets of `servers` sharded over `others` and this planet,
-    /// merged on this planet's device; records ascending by (key, rank).
-    pub fn search_topk(&self, others: &[&HipBote], servers: &[Region], clients: &[Region], n: usize,
-                       objectives: &[hip::bote_objective], k: usize, rp: &hip::bote_ranking_params)
-        -> (Vec<Vec<hip::bote_topk_record>>, u64, u64) {
+    /// The multi-GPU exhaustive search (bote_search_create/launch/result):
+    /// colex ranks of n-subsets of `servers` sharded over this planet and
+    /// `others`, merged on this planet's device; records ascending by
+    /// (key, rank).  All host work (shard bounds, chunk tables) happens in
+    /// `HipSearch::new`; every `run` is device work only.  `keys` selects the
+    /// key set (0: compute_stats' keys; 1: + Tempo tiny/write and FPaxos all
+    /// leaders, BASELINE config 5).
+    pub fn search<'b>(&'b self, others: &[&'b HipBote], servers: &[Region], clients: &[Region], n: usize,
+                      objectives: &[hip::bote_objective], k: usize, rp: &hip::bote_ranking_params, keys: u32)
+        -> HipSearch<'b> {
         let (s, c) = (self.ids(servers), self.ids(clients));
         let mut planets: Vec<*const hip::bote_planet> = vec![self.dev as *const _];
         planets.extend(others.iter().map(|b| b.dev as *const _));
         let total = unsafe { hip::bote_binomial(s.len() as u32, n as u32) };
-        let no = objectives.len();
+        let mut h: *mut hip::bote_search = std::ptr::null_mut();
+        hip::check(unsafe {
+            hip::bote_search_create(planets.as_ptr(), planets.len() as u32, s.as_ptr(), s.len() as u32, c.as_ptr(),
+                                    c.len() as u32, n as u32, 0, total, objectives.as_ptr(), objectives.len() as u32,
+                                    k as u32, rp, 1, keys, &mut h)
+        });
+        HipSearch { h, n_obj: objectives.len(), k, _planets: std::marker::PhantomData }
+    }
+
+    /// One-shot form (bote_search_topk): create, run once, destroy.
+    pub fn search_topk(&self, others: &[&HipBote], servers: &[Region], clients: &[Region], n: usize,
+                       objectives: &[hip::bote_objective], k: usize, rp: &hip::bote_ranking_params)
+        -> (Vec<Vec<hip::bote_topk_record>>, u64, u64) {
+        self.search(others, servers, clients, n, objectives, k, rp, 0).run()
+    }
+}
+
+/// A persistent multi-device search (bote_search_*); it borrows the planets.
+pub struct HipSearch<'a> {
+    h: *mut hip::bote_search,
+    n_obj: usize,
+    k: usize,
+    _planets: std::marker::PhantomData<&'a HipBote>,
+}
+
+impl<'a> HipSearch<'a> {
+    /// Launch every shard and the merge (device work only), then read the
+    /// merged top-K lists, the valid count and the digest.
+    pub fn run(&self) -> (Vec<Vec<hip::bote_topk_record>>, u64, u64) {
+        let (no, k) = (self.n_obj, self.k);
         let mut recs = vec![hip::bote_topk_record { key: 0, rank: 0 }; no * k];
         let mut cnt = vec![0u32; no];
         let (mut valid, mut digest) = (0u64, 0u64);
+        hip::check(unsafe { hip::bote_search_launch(self.h) });
         hip::check(unsafe {
-            hip::bote_search_topk(planets.as_ptr(), planets.len() as u32, s.as_ptr(), s.len() as u32, c.as_ptr(),
-                                  c.len() as u32, n as u32, 0, total, objectives.as_ptr(), no as u32, k as u32, rp,
-                                  1, recs.as_mut_ptr(), cnt.as_mut_ptr(), &mut valid, &mut digest)
+            hip::bote_search_result(self.h, recs.as_mut_ptr(), cnt.as_mut_ptr(), &mut valid, &mut digest)
         });
         let tops = (0..no).map(|o| recs[o * k..o * k + cnt[o] as usize].to_vec()).collect();
         (tops, valid, digest)
+    }
+}
+
+impl<'a> Drop for HipSearch<'a> {
+    fn drop(&mut self) {
+        unsafe {
+            hip::bote_search_destroy(self.h);
+        }
     }
 }
 

@@ -119,13 +119,38 @@ def make_windows(threads):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("what", nargs="?", default="all", choices=["topk", "windows", "all"])
+    ap.add_argument("what", nargs="?", default="all", choices=["topk", "windows", "all", "refresh_x"])
     ap.add_argument("--threads", type=int, default=8)
     a = ap.parse_args()
     if a.what in ("topk", "all"):
         make_topk(a.threads)
     if a.what in ("windows", "all"):
         make_windows(a.threads)
+    if a.what == "refresh_x":
+        make_topk(a.threads)
+        refresh_x(a.threads)
+
+
+
+def refresh_x(threads):
+    """Recompute the extended-key part of every fixture with the current
+    oracle and rewrite the entries that differ (used once after the digest's
+    definition changed while a generation was running)."""
+    p = Planet.synthetic(128)
+    path = os.path.join(HERE, "syn_r128n6_windows.json")
+    d = json.load(open(path))
+    changed = 0
+    for w in d["windows"]:
+        if "x" not in w:
+            continue
+        b, e = w["rank_begin"], w["rank_end"]
+        x = sweep_case(p, 6, b, e, objectives_x(6), 100, 1, threads)
+        if (x["valid"], x["digest"], x["tops"]) != (w["valid"], w["x"]["digest"], w["x"]["tops"]):
+            w["x"].update(digest=x["digest"], tops=x["tops"])
+            changed += 1
+        print("window", b, "x", "changed" if changed else "same", flush=True)
+    json.dump(d, open(path, "w"))
+    print("windows refreshed:", changed)
 
 
 if __name__ == "__main__":
