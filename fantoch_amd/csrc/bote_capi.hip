@@ -726,9 +726,6 @@ int bote_sweep_create_keys(const bote_planet* p, const uint32_t* servers, uint32
                                   BOTE_SLOT_E, BOTE_SLOT_TT1, BOTE_SLOT_TW2, BOTE_SLOT_FL1};
   for (uint32_t o = 0; keys_def && o < 8; ++o)
     keys_def = objs[o].kind == dkk[o] && (dkk[o] == BOTE_OBJ_SCORE || objs[o].slot == dss[o]);
-#ifndef BOTE_GROUP_BD
-#define BOTE_GROUP_BD 256
-#endif
   // (the group kernel's extended keys use 32-bit moments: every sum of
   // squares nc * (2 max)^2 and 3 nc max must fit their 32/24 bits)
   uint64_t maxlat_all = 0;
@@ -736,7 +733,7 @@ int bote_sweep_create_keys(const bote_planet* p, const uint32_t* servers, uint32
   const bool keys32 = (uint64_t)nc * (2 * maxlat_all) * (2 * maxlat_all) < (1ull << 32) &&
                       3ull * nc * maxlat_all < (1ull << 24);
   if (keys && s->fast &&
-      (!bote::group_supports_keys(n, BOTE_GROUP_BD) || !keys_def || !keys32 || kernel == BOTE_KERNEL_FAST)) {
+      (!bote::group_supports_keys(n, 256) || !keys_def || !keys32 || kernel == BOTE_KERNEL_FAST)) {
     if (kernel == BOTE_KERNEL_FAST || kernel == BOTE_KERNEL_GROUP)
       return cleanup(fail(BOTE_E_ARG, "the extended key set runs on the group kernel (n = 4..7, config 5's "
                                       "objectives) or the generic kernel"));
@@ -839,46 +836,75 @@ int bote_sweep_create_keys(const bote_planet* p, const uint32_t* servers, uint32
       // share the client-quad matrix, so R = 128 fits more waves per CU) were
       // measured slower: R=128 n=6 at 640 threads, 5 waves/SIMD, 369 ms vs
       // 348 ms at 256 threads, 2 waves/SIMD.
-#ifndef BOTE_GROUP_BD
-#define BOTE_GROUP_BD 256
-#endif
-      static_assert(BOTE_GROUP_BD % 64 == 0 && BOTE_GROUP_BD <= 1024, "group workgroup: 64..1024 threads");
-      f.gbd = BOTE_GROUP_BD;
-      // qtab member planes (non-PERM kernels): one u32 per thread, so the
-      // plane stride 1 << gqsh must hold gbd * 4 bytes (bote_group.hip)
-      f.gqsh = 10;
-      while ((1u << f.gqsh) < f.gbd * 4) ++f.gqsh;
-      f.gslots = 0;
-      f.grx = 0;
       // bote.py DEFAULT_OBJECTIVES: SCORE, MEAN af1, MEAN ff1, COV af1, MEAN e
       static const uint32_t dk[5] = {BOTE_OBJ_SCORE, BOTE_OBJ_MEAN, BOTE_OBJ_MEAN, BOTE_OBJ_COV, BOTE_OBJ_MEAN};
       static const uint32_t ds[5] = {0, BOTE_SLOT_AF1, BOTE_SLOT_FF1, BOTE_SLOT_AF1, BOTE_SLOT_E};
       s->def_obj = (keys ? keys_def : n_obj == 5) && f.want_score;
       for (uint32_t o = 0; s->def_obj && o < 5; ++o)
         s->def_obj = objs[o].kind == dk[o] && (dk[o] == BOTE_OBJ_SCORE || objs[o].slot == ds[o]);
-      if (bote::group_uses_lines(n)) {
-        // the per-group position table (n <= 7) unless its LDS lowers the
-        // workgroups per CU (R = 64: 4 either way, register-bound; R = 128:
-        // 3 without, 2 with it, measured 255 vs 280 ms)
-        const int occ_plain = bote::group_occupancy(f, n, bote::group_smem_bytes(f, n), s->def_obj);
-        f.grx = 1;
-        if (bote::group_occupancy(f, n, bote::group_smem_bytes(f, n), s->def_obj) < occ_plain) f.grx = 0;
-        // client lines per wave: as many (<= 16) as keep the workgroups per
-        // CU of the kernel without lines (a step has 7.7 distinct (p1, p2)
-        // on average at R=64 n=7, 4.0 at R=128 n=6)
-        const int occ0 = bote::group_occupancy(f, n, bote::group_smem_bytes(f, n), s->def_obj);
-        for (uint32_t sl = 16; sl >= 1; --sl) {
-          f.gslots = sl;
-          const size_t sh = bote::group_smem_bytes(f, n);
-          if (sh <= device_max_lds(p->device) && bote::group_occupancy(f, n, sh, s->def_obj) >= occ0) break;
-          f.gslots = 0;
+      // One geometry per candidate workgroup size: the position table (n <= 7)
+      // unless its LDS lowers the workgroups per CU, then as many client
+      // lines per wave (<= 16) as keep that occupancy.  A workgroup shares the
+      // client-quad matrix (CQT) among its waves, so at R = 128 larger
+      // workgroups leave LDS for the client lines that 256-thread ones cannot
+      // hold (a step has 7.7 distinct (p1, p2) on average at R=64 n=7, 4.0 at
+      // R=128 n=6).  pick_group_geometry keeps the best.
+      struct GGeo {
+        uint32_t bd = 0, grx = 0, gslots = 0, gqsh = 10;
+        int occ = 0;
+        size_t shm = 0;
+      };
+      auto geometry = [&](uint32_t bd) {
+        GGeo g;
+        g.bd = bd;
+        f.gbd = bd;
+        // qtab member planes (non-PERM kernels): one u32 per thread, so the
+        // plane stride 1 << gqsh must hold gbd * 4 bytes (bote_group.hip)
+        f.gqsh = 10;
+        while ((1u << f.gqsh) < f.gbd * 4) ++f.gqsh;
+        f.gslots = 0;
+        f.grx = 0;
+        if (bote::group_uses_lines(n)) {
+          const int occ_plain = bote::group_occupancy(f, n, bote::group_smem_bytes(f, n), s->def_obj);
+          f.grx = 1;
+          if (bote::group_occupancy(f, n, bote::group_smem_bytes(f, n), s->def_obj) < occ_plain) f.grx = 0;
+          const int occ0 = bote::group_occupancy(f, n, bote::group_smem_bytes(f, n), s->def_obj);
+          for (uint32_t sl = 16; sl >= 1; --sl) {
+            f.gslots = sl;
+            const size_t sh = bote::group_smem_bytes(f, n);
+            if (sh <= device_max_lds(p->device) && bote::group_occupancy(f, n, sh, s->def_obj) >= occ0) break;
+            f.gslots = 0;
+          }
         }
+        g.grx = f.grx;
+        g.gslots = f.gslots;
+        g.gqsh = f.gqsh;
+        g.shm = bote::group_smem_bytes(f, n);
+        g.occ = g.shm <= device_max_lds(p->device) ? bote::group_occupancy(f, n, g.shm, s->def_obj) : 0;
+        return g;
+      };
+      // candidates: multiples of 256 threads up to 1024 (the extended key
+      // set's kernels are bounded to bote::group_supports_keys' size).  Sizes
+      // of 6 or 10 waves put unequal wave counts on the 4 SIMDs of a CU
+      // (384 threads measured 16-21 % slower than both neighbours).
+      // BOTE_GROUP_BD (env) forces one size (A/B timing).
+      const char* bd_env = getenv("BOTE_GROUP_BD");
+      const uint32_t bd_only = bd_env ? (uint32_t)strtoul(bd_env, nullptr, 0) : 0u;
+      GGeo best;
+      for (uint32_t bd = 256; bd <= 1024; bd += 128) {
+        if (bd_only ? bd != bd_only : bd % 256 != 0) continue;
+        if (keys && !bote::group_supports_keys(n, bd)) continue;
+        const GGeo g = geometry(bd);
+        if (g.occ > 0 && bote::host::pick_group_geometry(g.bd, g.occ, g.gslots, best.bd, best.occ, best.gslots)) best = g;
       }
-      const size_t gshm = bote::group_smem_bytes(f, n);
-      if (gshm <= device_max_lds(p->device) && (!keys || s->def_obj)) {
+      if (best.occ > 0 && (!keys || s->def_obj)) {
+        f.gbd = best.bd;
+        f.grx = best.grx;
+        f.gslots = best.gslots;
+        f.gqsh = best.gqsh;
         s->group = true;
-        s->fshm = gshm;
-        s->fgrid = (uint32_t)(device_cus(p->device) * std::max(1, bote::group_occupancy(f, n, gshm, s->def_obj)));
+        s->fshm = best.shm;
+        s->fgrid = (uint32_t)(device_cus(p->device) * best.occ);
       }
     }
   }

@@ -338,11 +338,11 @@ __device__ __forceinline__ float u64_to_f32(uint64_t x) {
 // through the client loop: its kernels target 3 waves per SIMD (<= 168
 // VGPRs); config 5 (R = 128) is LDS-bound at 3 workgroups per CU anyway.
 // (a 1024-thread bound would cap registers at 128 whatever the wave target:
-// the XK kernels are bounded to 256-thread workgroups)
+// the XK kernels are bounded to 768-thread workgroups, 3 waves per SIMD each)
 #ifndef BOTE_GROUP_WAVES_XK
 #define BOTE_GROUP_WAVES_XK 3
 #endif
-constexpr uint32_t GROUP_XK_MAX_BD = 256;
+constexpr uint32_t GROUP_XK_MAX_BD = 768;
 // client-loop quads per iteration of the base kernels (a build knob)
 #ifndef BOTE_GROUP_UNROLL
 #define BOTE_GROUP_UNROLL 4

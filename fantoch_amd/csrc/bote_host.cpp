@@ -170,6 +170,24 @@ double group_utilisation(uint32_t ns, uint32_t n) {
   return steps > 0 ? (double)(cfg / (64 * steps)) : 0.0;
 }
 
+bool pick_group_geometry(uint32_t bd, int occ, uint32_t gslots, uint32_t best_bd, int best_occ,
+                         uint32_t best_gslots) {
+  if (occ <= 0) return false;
+  if (best_occ <= 0) return true;
+  // client lines for most steps first (up to 8 per wave: a step has 7.7
+  // distinct (p1, p2) on average at R=64 n=7, 4.0 at R=128 n=6), then more
+  // waves per CU, more client lines, the smaller size.  Measured at R=128
+  // n=6: 10 keys 203.4 ms at 256 threads (3 workgroups per
+  // CU, 4 lines) vs 183.3 ms at 512 (2 per CU, 16 lines); extended keys
+  // 389.2 ms at 256 (no lines) vs 351.5 ms at 512 (1 per CU, 16 lines)
+  const uint32_t c = std::min<uint32_t>(gslots, 8), bc = std::min<uint32_t>(best_gslots, 8);
+  if (c != bc) return c > bc;
+  const uint32_t w = (uint32_t)occ * (bd / 64), bw = (uint32_t)best_occ * (best_bd / 64);
+  if (w != bw) return w > bw;
+  if (gslots != best_gslots) return gslots > best_gslots;
+  return bd < best_bd;
+}
+
 std::vector<uint16_t> quad_layout(const uint16_t* lat, uint32_t R, const uint32_t* rows, uint32_t nrows,
                                   uint32_t shift, uint32_t& quads) {
   quads = (nrows + 3) / 4;

@@ -50,6 +50,11 @@ std::shared_ptr<GroupWalk> walk_groups(uint32_t ns, uint32_t n, uint32_t nc, uin
 std::vector<uint64_t> cut_chunks(const GroupWalk& w, uint64_t b, uint64_t e, uint32_t nchunks);
 // Expected lane utilisation of the group kernel over the whole rank space.
 double group_utilisation(uint32_t ns, uint32_t n);
+// Group-kernel geometry choice between two workgroup sizes, each with the
+// workgroups per CU (occ) and client lines per wave (gslots) it fits: true
+// when (bd, occ, gslots) should replace the best so far (best_occ == 0: none).
+bool pick_group_geometry(uint32_t bd, int occ, uint32_t gslots, uint32_t best_bd, int best_occ,
+                         uint32_t best_gslots);
 
 // ------------------------------------------------------------ layouts ----
 // Column-major packed-u16 quad layout of `rows` (client ids) against every
