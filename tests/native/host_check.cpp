@@ -211,7 +211,24 @@ static void check_unpack() {
   unpack_result(blk.data(), n_obj, K, kp, nullptr, nullptr, nullptr, nullptr);  // all outputs optional
 }
 
+// The group geometry choice (bote_capi.hip): client-line coverage up to 8
+// per wave first, then waves per CU, then more lines, then the smaller size;
+// checked on the three measured R=128/R=64 cases.
+static void check_geometry() {
+  // R=64 n=7: 256 x 4 per CU vs 512 x 2, both 16 lines -> 256
+  CHECK(pick_group_geometry(256, 4, 16, 0, 0, 0));
+  CHECK(!pick_group_geometry(512, 2, 16, 256, 4, 16));
+  // R=128 10 keys: 256 x 3 with 4 lines vs 512 x 2 with 16 -> 512
+  CHECK(pick_group_geometry(512, 2, 16, 256, 3, 4));
+  // extended keys: 256 x 3 without lines, 512 x 1, 768 x 1 (16 lines) -> 768
+  CHECK(pick_group_geometry(512, 1, 16, 256, 3, 0));
+  CHECK(pick_group_geometry(768, 1, 16, 512, 1, 16));
+  CHECK(!pick_group_geometry(1024, 0, 16, 768, 1, 16));  // does not fit
+  CHECK(!pick_group_geometry(256, 0, 0, 0, 0, 0));
+}
+
 int main() {
+  check_geometry();
   check_binomials();
   check_unrank();
   check_walk();
