@@ -888,19 +888,29 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
           uint32_t bi = 0;
           bool amb = false;
           if (!ABLATE(a, 128)) {
-            float tl[N];
+            // t >= 0 and never NaN here (S >= nc * Q2 > 0: server-server
+            // latencies are > 0 on the fast path, so Q2 > 0).  Non-negative
+            // floats order as their bit patterns, so each t's low IB mantissa
+            // bits carry IM - l instead (a change below 2^-19 relative, inside
+            // the band below): the integer max is the largest t with the
+            // FIRST member on exact ties, and no compare/select chain is needed.
+            constexpr uint32_t IM = N <= 8 ? 7u : 15u;
+            uint32_t u[N];
 #pragma unroll
-            for (int l = 0; l < N; ++l) tl[l] = (float)(s1_of(l) + __umul24(nc, Q2[l])) * wf_of(l);
+            for (int l = 0; l < N; ++l) {
+              const float t = (float)(s1_of(l) + __umul24(nc, Q2[l])) * wf_of(l);
+              u[l] = (__float_as_uint(t) & ~IM) | (IM - (uint32_t)l);
+            }
             // the largest and second largest (with multiplicity) t: a
             // running max and median-of-three, 2 ops per member
-            float m = tl[0], m2 = -1.0f;
+            uint32_t mu = u[0], m2u = 0;
 #pragma unroll
             for (int l = 1; l < N; ++l) {
-              m2 = __builtin_amdgcn_fmed3f(m, m2, tl[l]);
-              m = fmaxf(m, tl[l]);
+              m2u = max(min(mu, m2u), min(max(mu, m2u), u[l]));  // (v_med3_u32)
+              mu = max(mu, u[l]);
             }
-#pragma unroll
-            for (int l = N - 1; l >= 0; --l) bi = tl[l] == m ? (uint32_t)l : bi;  // the first at m
+            bi = (mu & IM) ^ IM;  // the first member at the maximum
+            const float m = __uint_as_float(mu & ~IM), m2 = __uint_as_float(m2u & ~IM);
             amb = m < __builtin_inff() && m2 >= m * (1.0f - 0x1p-18f);
           }
           if (amb) {  // exact re-scan in the generic path's arithmetic
@@ -1265,12 +1275,14 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
                     const uint64_t ob = ~tkey;
                     const uint64_t bits = (ob >> 63) ? (ob & 0x7FFFFFFFFFFFFFFFull) : ~ob;
                     const double tscore = __longlong_as_double((long long)bits);
-                    int64_t T = 0;
+                    // (32-bit: every S1 here is below 2^21, so |T| < 2^27)
+                    int32_t T = 0;
 #pragma unroll
                     for (int f = 1; f <= 2; ++f) {
                       if (f > fcap) break;
-                      const int64_t a1 = (int64_t)mom[f == 1 ? SLOT_AF1 : SLOT_AF2].s1;
-                      T += (int64_t)mom[f == 1 ? SLOT_FF1 : SLOT_FF2].s1 - a1 + 30 * ((int64_t)mom[SLOT_E].s1 - a1);
+                      const int32_t a1 = (int32_t)(uint32_t)mom[f == 1 ? SLOT_AF1 : SLOT_AF2].s1;
+                      T += (int32_t)(uint32_t)mom[f == 1 ? SLOT_FF1 : SLOT_FF2].s1 - a1 +
+                           30 * ((int32_t)(uint32_t)mom[SLOT_E].s1 - a1);
                     }
                     maybe = !(tscore == tscore) || (double)T >= (tscore - 1e-6) * (double)nc;
                   }
