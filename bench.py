@@ -326,7 +326,7 @@ def main():
 
     from fantoch_amd import _lib
     from fantoch_amd.bote import CONFIG5_OBJECTIVES, DEFAULT_OBJECTIVES, DEFAULT_RANKING, DevicePlanet, Sweep
-    from fantoch_amd.dist import shard_of, sharded_sweep, world_census
+    from fantoch_amd.dist import shard_of, sharded_sweep_start, world_census
     from fantoch_amd.planet import Planet
 
     wl = workloads()[args.workload]
@@ -342,18 +342,28 @@ def main():
     b, e = shard_of(sweep, world, rank)  # equal estimated cost (bote_sweep_split)
     stream = torch.cuda.current_stream().cuda_stream
 
-    def step():
-        return sharded_sweep(sweep, stream)
+    # Steps are pipelined: step i+1 is enqueued (launch, all-gather, merge,
+    # copy of the merged block to pinned host memory) before the host parses
+    # step i's result, so the device never waits for the host.  Every step's
+    # full result is produced and parsed inside the timed region.
+    hosts = [torch.empty(sweep.result_bytes(), dtype=torch.uint8, pin_memory=True) for _ in range(2)]
 
-    for _ in range(args.warmup):
-        res = step()
+    def run(k):
+        pend, res = None, None
+        for i in range(k):
+            nxt = sharded_sweep_start(sweep, stream, host=hosts[i % 2])
+            if pend is not None:
+                res = pend.result()
+            pend = nxt
+        return pend.result() if pend is not None else res
+
+    res = run(args.warmup)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     sweep.timing_reset()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        res = step()
+    res = run(args.steps)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

@@ -411,6 +411,15 @@ __global__ void __launch_bounds__(256) eval_kernel(EvalArgs a) {
   const Smem s = carve<N>(a, smem, NLW);
   const uint32_t BD = blockDim.x, tid = threadIdx.x;
   const bool topk = !FULL && a.out_top != nullptr;
+  if (a.rank_list && *a.rank_count == 0) {
+    // the deferred-config fix-up with nothing deferred (the common case):
+    // empty lists for the merge, nothing staged (block-uniform)
+    if (topk) {
+      Rec* dst = a.out_top + (size_t)blockIdx.x * a.n_obj * KP;
+      for (uint32_t i = tid; i < (uint32_t)a.n_obj * KP; i += BD) dst[i] = rec_max();
+    }
+    return;
+  }
 
   // stage the planet, client offsets, server list, column sums, binomials
   for (uint32_t i = tid; i < a.R * a.R; i += BD) s.mat[i] = a.mat[i];

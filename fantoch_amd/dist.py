@@ -55,6 +55,28 @@ def sharded_sweep(sweep, stream=None, group=None, device=None):
     result_device(ptr, stream), merge_device(src_ptr, n, dst_ptr, stream) and
     parse_block(np.ndarray); the blocks live on `device` (default: the GPU of
     the sweep's planet, whose current stream is used)."""
+    return sharded_sweep_start(sweep, stream, group, device).result()
+
+
+class PendingSweep:
+    """A sharded sweep enqueued on the device (launch, all-gather, merge and
+    the copy of the merged block to pinned host memory, all stream-ordered):
+    result() waits for that copy only, so the host can enqueue the next sweep
+    first and parse this one while the device runs it."""
+
+    def __init__(self, sweep, host, event):
+        self.sweep, self.host, self.event = sweep, host, event
+
+    def result(self):
+        if self.event is not None:
+            self.event.synchronize()
+        return self.sweep.parse_block(self.host.numpy())
+
+
+def sharded_sweep_start(sweep, stream=None, group=None, device=None, host=None) -> PendingSweep:
+    """Enqueue sharded_sweep without waiting for it.  `host`: a pinned uint8
+    CPU tensor of sweep.result_bytes() to copy the merged block into (one per
+    sweep in flight; allocated when None)."""
     import torch
     import torch.distributed as dist
 
@@ -68,23 +90,33 @@ def sharded_sweep(sweep, stream=None, group=None, device=None):
     nbytes = sweep.result_bytes()
     blk = torch.empty(nbytes, dtype=torch.uint8, device=device)
     sweep.result_device(blk.data_ptr(), stream)
-    if world == 1:
-        return sweep.parse_block(blk.cpu().numpy())
-    if device.type == "cuda" and dist.get_backend(group) == "gloo":
-        # gloo moves host memory: gather through the host (a rehearsal of
-        # the N-rank path with several ranks on one GPU; RCCL gathers on the device)
-        g = torch.empty(world * nbytes, dtype=torch.uint8)
-        dist.all_gather_into_tensor(g, blk.cpu(), group=group)
-        gathered = g.to(device)
-    else:
-        gathered = torch.empty(world * nbytes, dtype=torch.uint8, device=device)
-        dist.all_gather_into_tensor(gathered, blk, group=group)
-    return merge_gathered(sweep, gathered, world, stream, device)
+    if world > 1:
+        if device.type == "cuda" and dist.get_backend(group) == "gloo":
+            # gloo moves host memory: gather through the host (a rehearsal of
+            # the N-rank path with several ranks on one GPU; RCCL gathers on the device)
+            g = torch.empty(world * nbytes, dtype=torch.uint8)
+            dist.all_gather_into_tensor(g, blk.cpu(), group=group)
+            gathered = g.to(device)
+        else:
+            gathered = torch.empty(world * nbytes, dtype=torch.uint8, device=device)
+            dist.all_gather_into_tensor(gathered, blk, group=group)
+        blk = merge_gathered_device(sweep, gathered, world, stream, device)
+    if device.type != "cuda":
+        return PendingSweep(sweep, blk, None)
+    if host is None:
+        host = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
+    cur = torch.cuda.current_stream(device)
+    st = cur if stream in (None, 0, cur.cuda_stream) else torch.cuda.ExternalStream(stream, device=device)
+    with torch.cuda.stream(st):
+        host.copy_(blk, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+    return PendingSweep(sweep, host, ev)
 
 
-def merge_gathered(sweep, gathered, world: int, stream=None, device=None):
+def merge_gathered_device(sweep, gathered, world: int, stream=None, device=None):
     """Deterministic merge of `world` concatenated result blocks (the all-gather
-    output, rank order) into one result; every rank runs it on its own copy."""
+    output, rank order) into one result block on the device (stream-ordered)."""
     import torch
 
     device = _device_of(sweep, device)
@@ -100,7 +132,12 @@ def merge_gathered(sweep, gathered, world: int, stream=None, device=None):
             sweep.merge_device(src.data_ptr() + 8 * g * nbytes, k, nxt.data_ptr() + g * nbytes, stream)
         src, n = nxt, groups
     sweep.merge_device(src.data_ptr(), n, out.data_ptr(), stream)
-    return sweep.parse_block(out.cpu().numpy())
+    return out
+
+
+def merge_gathered(sweep, gathered, world: int, stream=None, device=None):
+    """merge_gathered_device, then the merged result on the host."""
+    return sweep.parse_block(merge_gathered_device(sweep, gathered, world, stream, device).cpu().numpy())
 
 
 def world_census(device=None, group=None):
