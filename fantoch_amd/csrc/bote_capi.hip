@@ -730,8 +730,13 @@ int bote_sweep_create_keys(const bote_planet* p, const uint32_t* servers, uint32
   // squares nc * (2 max)^2 and 3 nc max must fit their 32/24 bits)
   uint64_t maxlat_all = 0;
   for (auto v : p->lat) maxlat_all = std::max<uint64_t>(maxlat_all, v);
+  // (and its member bins: a client count below 2^8, a sum of nc keys
+  // (latency << 4 | member) below 2^24 and two squared keys below 2^32,
+  // bote_group.hip)
   const bool keys32 = (uint64_t)nc * (2 * maxlat_all) * (2 * maxlat_all) < (1ull << 32) &&
-                      3ull * nc * maxlat_all < (1ull << 24);
+                      3ull * nc * maxlat_all < (1ull << 24) && nc < 256 &&
+                      (uint64_t)nc * (16 * maxlat_all + 15) < (1ull << 24) &&
+                      2 * (16 * maxlat_all + 15) * (16 * maxlat_all + 15) < (1ull << 32);
   if (keys && s->fast &&
       (!bote::group_supports_keys(n, 256) || !keys_def || !keys32 || kernel == BOTE_KERNEL_FAST)) {
     if (kernel == BOTE_KERNEL_FAST || kernel == BOTE_KERNEL_GROUP)
@@ -775,6 +780,10 @@ int bote_sweep_create_keys(const bote_planet* p, const uint32_t* servers, uint32
     // packed-u16 sums (group kernel): each half gains <= 2 * amax per quad
     const uint64_t s1_flush = amax ? 0xFFFFull / (2 * amax) : 1u << 20;
     f.g_flush = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(f.s2_flush, s1_flush));
+    // extended keys: squares of the packed keys (latency << 4 | member), two
+    // per dot2 into 32 bits (keys32 below requires 2 key^2 < 2^32)
+    const uint64_t kmax = 16ull * maxlat + 15, kq = 4 * kmax * kmax;
+    f.k_flush = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(1u << 20, 0xFFFFFFFFull / kq));
     f.want_score = a.want_score;
     f.p_fmean = a.p_fmean;
     f.p_emean = a.p_emean;
@@ -1075,8 +1084,6 @@ static int launch_fast_path(bote_sweep* s, uint64_t rb, uint64_t re, hipStream_t
   const uint64_t count = re - rb;
   const uint64_t G = (uint64_t)s->fgrid * bote::FAST_BD;
   f.runlen = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(32, count / (G * 8)));
-  HIP_TRY(hipMemsetAsync(s->counters.p, 0, 16, st));
-  HIP_TRY(hipMemsetAsync(s->qcount.p, 0, 8, st));
   if (s->group) {
     // cost-balanced chunks (32 per wave), taken dynamically (bote_group.hip)
     const bote_sweep::Chunks* ch = nullptr;
@@ -1087,9 +1094,11 @@ static int launch_fast_path(bote_sweep* s, uint64_t rb, uint64_t re, hipStream_t
     if (f.nwchunks) {
       if (!s->wctr.p && s->wctr.alloc(16) != hipSuccess) return fail(BOTE_E_NOMEM, "hipMalloc work counter");
       f.wctr = s->wctr.as<unsigned int>();
-      HIP_TRY(hipMemsetAsync(s->wctr.p, 0, 4, st));
     }
   }
+  // counters, deferred count, work tickets, fallback counters: one launch
+  HIP_TRY(bote::launch_zero_ctl(s->counters.as<unsigned long long>(), s->qcount.as<unsigned long long>(),
+                                f.nwchunks ? f.wctr : nullptr, s->counters_alt.as<unsigned long long>(), st));
   hipEvent_t *e0 = nullptr, *e1 = nullptr;
   int rc;
   if ((rc = timing_slot(s, e0, e1))) return rc;
@@ -1121,7 +1130,6 @@ static int launch_fast_path(bote_sweep* s, uint64_t rb, uint64_t re, hipStream_t
   g.out_counters = s->counters_alt.as<unsigned long long>();
   g.run_if_over = s->qcount.as<unsigned long long>();
   g.over_cap = QUEUE_CAP;
-  HIP_TRY(hipMemsetAsync(s->counters_alt.p, 0, 16, st));
   HIP_TRY(bote::launch_eval(g, s->n, false, s->grid, s->bd, s->shm, st));
   return merge_chain(s, s->fgrid + s->xgrid, st, s->qcount.as<unsigned long long>(), s->grid);
 }
@@ -1147,7 +1155,8 @@ int bote_sweep_result_device(bote_sweep* s, void* dst, void* hip_stream) {
   if (!s || !dst) return fail(BOTE_E_ARG, "null argument");
   if (!s->launched) return fail(BOTE_E_ARG, "sweep not launched");
   HIP_TRY(hipSetDevice(s->p->device));
-  HIP_TRY(hipMemcpyAsync(dst, s->result.p, s->result_bytes(), hipMemcpyDeviceToDevice, (hipStream_t)hip_stream));
+  // (dst: device memory, or pinned host memory: the direct device-to-host copy)
+  HIP_TRY(hipMemcpyAsync(dst, s->result.p, s->result_bytes(), hipMemcpyDefault, (hipStream_t)hip_stream));
   return BOTE_OK;
 }
 

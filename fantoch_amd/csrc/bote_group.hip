@@ -122,12 +122,16 @@ __host__ __device__ inline size_t group_layout(const FastArgs& a, int N, int NLW
   off[11] = o; o += (size_t)a.K * 16;          // tmp
   off[12] = o; o += (size_t)MAXOBJ * 16;      // thr
   off[13] = o; o += 48;                       // lock
+  // extended key set (PERM kernels): per wave, N member bins of 64 lanes' u32
+  // (the client loop's binned sums, sweep_group_kernel)
+  o = (o + 15) & ~(size_t)15;
+  off[14] = o; o += perm && a.keys ? (size_t)(a.gbd / 64) * N * 256 : 0;
   return o;
 }
 
 template <int N>
 static size_t group_smem_n(const FastArgs& a) {
-  size_t off[14];
+  size_t off[15];
   return group_layout(a, N, QCfg<N>::NL <= 2 ? 1 : 2, GCfg<N>::KQ, GCfg<N>::PERM, off);
 }
 
@@ -368,7 +372,7 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
   using QT = QTab<N, XK>;
   constexpr int NT = QT::NT;  // leaderless tables (PERM: register byte planes); == NL without XK
   extern __shared__ __align__(16) unsigned char smem[];
-  size_t off[14];
+  size_t off[15];
   group_layout(a, N, NLW, KQ, PERM, off);
   const uint32_t LB = lds_base(smem);
   const uint32_t qtab = LB + (uint32_t)off[0];
@@ -406,6 +410,9 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
   for (uint32_t i = tid; i < (uint32_t)a.n_obj * a.K; i += BD) tk.top[i] = rec_max();
   if (tid < MAXOBJ) tk.thr[tid] = rec_max();
   if (tid == 0) *lock = 0;
+  // XK: the member bins start at zero (each lane re-zeroes its own after use)
+  if constexpr (XK)
+    for (uint32_t i = tid; i < (BD >> 6) * N * 64; i += BD) ((uint32_t*)(smem + off[14]))[i] = 0;
   __syncthreads();
   const uint32_t cstride = (a.cq_quads + 1) * 8;  // bytes per CQT column
   const uint32_t rstride = (a.rq_quads + 1) * 8;
@@ -853,10 +860,12 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
 #pragma unroll
             for (int t = 0; t < NT; ++t) {
               const uint32_t w01 = wp[t][0], w2 = wp[t][1], w34 = wp[t][2], w56 = FP >= 2 ? wp[t][FP >= 2 ? 3 : 2] : 0u;
-              QL[t].x = __builtin_amdgcn_perm(w2, w01, 0x0C040200u) | (w34 << 24);
-              QH[t].x = __builtin_amdgcn_perm(w34, __builtin_amdgcn_perm(w2, w01, 0x0C050301u), 0x05020100u);
-              QL[t].y = __builtin_amdgcn_perm(w56, w34, 0x0C060402u);
-              QH[t].y = __builtin_amdgcn_perm(w56, w34, 0x0C070503u);
+              if constexpr (!XK) {  // (XK bins the clients by member instead)
+                QL[t].x = __builtin_amdgcn_perm(w2, w01, 0x0C040200u) | (w34 << 24);
+                QH[t].x = __builtin_amdgcn_perm(w34, __builtin_amdgcn_perm(w2, w01, 0x0C050301u), 0x05020100u);
+                QL[t].y = __builtin_amdgcn_perm(w56, w34, 0x0C060402u);
+                QH[t].y = __builtin_amdgcn_perm(w56, w34, 0x0C070503u);
+              }
               uint32_t ps = 0, sq = 0;
 #pragma unroll
               for (int i = 0; i < 2 + FP; ++i) {
@@ -1128,8 +1137,137 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
                   flush();
                 }
               };
-              if (PERM && use_lines) clients(BoolC<PERM>{});
-              else clients(BoolC<false>{});
+              if constexpr (XK) {
+                // ---- XK: the clients binned by nearest member, so the loop
+                //      does not depend on the number of tables (4 here).  Per
+                //      client one LDS add of (key | 1 << 24) into its member's
+                //      bin (this lane's word of member m at bin + 256 m): the
+                //      bin holds cnt_m (bits 24..31) and K_m, the sum of keys
+                //      (latency << 4 | m) of the member's clients = 16 D1_m +
+                //      m cnt_m.  Then per table t, exactly,
+                //        S1_t = L1 + sum_m cnt_m q_t[m],
+                //        S2_t = L2 + 2 sum_m D1_m q_t[m] + sum_m cnt_m q_t[m]^2
+                //      (L1 = sum of latencies = sum_m D1_m, L2 = sum of squares).
+                //      The host runs this only where the fields cannot overflow
+                //      (nc < 256, nc (16 max + 15) < 2^24; bote_capi.hip).
+                const uint32_t bin = LB + (uint32_t)off[14] + wid * (N * 256) + lane * 4;
+                uint32_t s2l = 0;
+                uint64_t L2 = 0;
+                auto badd = [&](uint32_t addr, uint32_t v) {
+                  __hip_atomic_fetch_add((AS3 uint32_t*)(uintptr_t)addr, v, __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_WAVEFRONT);
+                };
+                // bin address of a client's member tag t: bin + (t << 8) in one
+                // v_lshl_add (the compiler would emit shift, and, add)
+                auto baddr = [&](uint32_t t) {
+                  uint32_t r;
+                  asm("v_lshl_add_u32 %0, %1, 8, %2" : "=v"(r) : "v"(t), "v"(bin));
+                  return r;
+                };
+                // (the keys of a group of quads are read before any of their
+                // bin adds: the compiler cannot tell the bins from the CQT and
+                // lines, so it keeps program order between LDS reads and adds)
+                auto quad_keys = [&](auto lines_c, uint32_t g8, uint32_t& L, uint32_t& H) {
+                  us2 lo, hi;
+                  nearest(lines_c, g8, lo, hi);
+                  L = as_u32(lo);
+                  H = as_u32(hi);
+                };
+                auto quad_bin = [&](uint32_t L, uint32_t H, uint32_t nv) {
+#ifdef BOTE_DEBUG
+                  GASSERT(a, (L & 15u) < (uint32_t)N && ((L >> 16) & 15u) < (uint32_t)N && (H & 15u) < (uint32_t)N &&
+                                 ((H >> 16) & 15u) < (uint32_t)N, 8);
+#endif
+                  if (nv < 4) {  // (the last, partial quad: uniform)
+                    L &= nv >= 2 ? ~0u : 0x0000FFFFu;
+                    H &= nv == 3 ? 0x0000FFFFu : 0u;
+                  }
+                  // squared keys (16 lat + m)^2 = 256 lat^2 + 32 lat m + m^2:
+                  // L2 follows from their sum and the bins (below)
+                  s2l = __builtin_amdgcn_udot2(as_us2(L), as_us2(L), s2l, false);
+                  s2l = __builtin_amdgcn_udot2(as_us2(H), as_us2(H), s2l, false);
+                  badd(baddr(L & 15u), __builtin_amdgcn_perm(0x01000000u, L, 0x070C0100u));
+                  if (nv >= 2) badd(baddr(__builtin_amdgcn_ubfe(L, 16, 4)), __builtin_amdgcn_perm(0x01000000u, L, 0x070C0302u));
+                  if (nv >= 3) badd(baddr(H & 15u), __builtin_amdgcn_perm(0x01000000u, H, 0x070C0100u));
+                  if (nv >= 4) badd(baddr(__builtin_amdgcn_ubfe(H, 16, 4)), __builtin_amdgcn_perm(0x01000000u, H, 0x070C0302u));
+                };
+                auto clients_bin = [&](auto lines_c) {
+                  // s2l (squared keys) is flushed to 64 bits every k_flush quads
+                  constexpr uint32_t UB = 4;
+                  const uint32_t fU = a.k_flush / UB ? a.k_flush / UB : 1u;
+                  uint32_t g = 0, k = 0;
+                  if (a.k_flush >= UB) {
+                    for (; g + UB <= nql; g += UB) {
+                      uint32_t Lk[UB], Hk[UB];
+#pragma unroll
+                      for (uint32_t u = 0; u < UB; ++u) quad_keys(lines_c, g * 8 + 8 * u, Lk[u], Hk[u]);
+#pragma unroll
+                      for (uint32_t u = 0; u < UB; ++u) quad_bin(Lk[u], Hk[u], 4u);
+                      if (++k == fU) {
+                        L2 += s2l;
+                        s2l = 0;
+                        k = 0;
+                      }
+                    }
+                    L2 += s2l;
+                    s2l = 0;
+                  }
+                  for (; g < nql; ++g) {
+                    uint32_t Lk, Hk;
+                    quad_keys(lines_c, g * 8, Lk, Hk);
+                    quad_bin(Lk, Hk, 4u);
+                    L2 += s2l;
+                    s2l = 0;
+                  }
+                  if (rem && !ABLATE(a, 1)) {
+                    uint32_t Lk, Hk;
+                    quad_keys(lines_c, nq * 8, Lk, Hk);
+                    quad_bin(Lk, Hk, rem);
+                  }
+                  L2 += s2l;
+                };
+                if (use_lines) clients_bin(BoolC<true>{});
+                else clients_bin(BoolC<false>{});
+                // the bins (re-zeroed for the next config of this lane)
+                uint32_t cnt[N], D1[N], L1 = 0;
+                uint64_t corr = 0;  // 32 sum_m m D1_m + sum_m m^2 cnt_m
+#pragma unroll
+                for (int m = 0; m < N; ++m) {
+                  const uint32_t w = l32(bin + 256u * m);
+                  s32(bin + 256u * m, 0u);
+                  cnt[m] = w >> 24;
+                  D1[m] = ((w & 0xFFFFFFu) - (uint32_t)m * cnt[m]) >> 4;
+                  L1 += D1[m];
+                  if (m) corr += (uint64_t)(32u * m) * D1[m] + (uint32_t)(m * m) * cnt[m];
+                }
+                L2 = (L2 - corr) >> 8;  // exact: the sum of squared keys is 256 L2 + corr
+#pragma unroll
+                for (int t = 0; t < NT; ++t) {
+                  // member m's quorum latency in table t (wp: the packed rows)
+                  uint32_t qv[N];
+                  qv[0] = wp[t][0] & 0xFFFFu;
+                  qv[1] = wp[t][0] >> 16;
+                  qv[2] = wp[t][1] & 0xFFFFu;
+#pragma unroll
+                  for (int m = 3; m < N; ++m) {
+                    const uint32_t w = wp[t][2 + (m - 3) / 2];
+                    qv[m] = ((m - 3) & 1) ? w >> 16 : w & 0xFFFFu;
+                  }
+                  uint32_t s1 = L1, x = 0, qq = 0;
+#pragma unroll
+                  for (int m = 0; m < N; ++m) {
+                    const uint32_t cq = __umul24(cnt[m], qv[m]);
+                    s1 += cq;
+                    qq = __umul24(cq, qv[m]) + qq;
+                    x = __umul24(D1[m], qv[m]) + x;
+                  }
+                  S1[t] = s1;
+                  S2[t] = L2 + ((uint64_t)x << 1) + qq;
+                }
+              } else {
+                if (PERM && use_lines) clients(BoolC<PERM>{});
+                else clients(BoolC<false>{});
+              }
               if (ABLATE(a, 1)) {  // timing only: non-degenerate dummy sums
 #pragma unroll
                 for (int t = 0; t < NT; ++t) {

@@ -787,6 +787,24 @@ __global__ void pick_counters_kernel(const unsigned long long* src, const unsign
   if (threadIdx.x < 2) dst[threadIdx.x] = (*sel > cap ? alt : src)[threadIdx.x];
 }
 
+// the per-launch control words of a fast-path sweep zeroed in one launch
+// (valid/digest counters, the deferred-queue count, the work-ticket counter,
+// the overflow fallback's counters) instead of four memsets
+__global__ void zero_ctl_kernel(unsigned long long* counters, unsigned long long* qcount, unsigned int* wctr,
+                                unsigned long long* counters_alt) {
+  const uint32_t t = threadIdx.x;
+  if (t < 2) counters[t] = 0;
+  if (t == 2) *qcount = 0;
+  if (t == 3 && wctr) *wctr = 0;
+  if (t >= 4 && t < 6) counters_alt[t - 4] = 0;
+}
+
+hipError_t launch_zero_ctl(unsigned long long* counters, unsigned long long* qcount, unsigned int* wctr,
+                           unsigned long long* counters_alt, hipStream_t st) {
+  hipLaunchKernelGGL(zero_ctl_kernel, dim3(1), dim3(64), 0, st, counters, qcount, wctr, counters_alt);
+  return hipGetLastError();
+}
+
 hipError_t launch_pick_counters(const unsigned long long* src, const unsigned long long* alt,
                                 const unsigned long long* sel, uint64_t cap, uint64_t* dst, hipStream_t st) {
   hipLaunchKernelGGL(pick_counters_kernel, dim3(1), dim3(64), 0, st, src, alt, sel, cap, dst);

@@ -95,6 +95,7 @@ struct FastArgs {
   uint32_t runlen;
   uint32_t s2_flush;  // quads per 32-bit sum-of-squares chunk
   uint32_t g_flush;   // group kernel: quads per flush of its 32-bit square sums and packed-u16 sums
+  uint32_t k_flush;   // group kernel, extended keys: quads per flush of its 32-bit sum of squared keys
   uint32_t gbd;       // group kernel: workgroup size (multiple of 64, <= 1024)
   uint32_t gqsh;      // group kernel: log2 of the qtab plane stride in bytes (1 << gqsh >= gbd * 4)
   uint32_t gslots;    // group kernel, n <= 7: client lines per wave (0: none), see bote_group.hip
@@ -183,6 +184,8 @@ hipError_t launch_merge_sel(const Rec* src, uint32_t n_lists, const Rec* alt, ui
                             const unsigned long long* sel, uint64_t cap, Rec* dst, uint64_t out_stride, uint32_t n_obj,
                             hipStream_t st);
 // dst[0..1] = (*sel > cap ? alt : src)[0..1]
+hipError_t launch_zero_ctl(unsigned long long* counters, unsigned long long* qcount, unsigned int* wctr,
+                           unsigned long long* counters_alt, hipStream_t st);
 hipError_t launch_pick_counters(const unsigned long long* src, const unsigned long long* alt,
                                 const unsigned long long* sel, uint64_t cap, uint64_t* dst, hipStream_t st);
 

@@ -88,6 +88,15 @@ def sharded_sweep_start(sweep, stream=None, group=None, device=None, host=None) 
         stream = torch.cuda.current_stream(device).cuda_stream
     sweep.launch(b, e, stream)
     nbytes = sweep.result_bytes()
+    if world == 1 and device.type == "cuda":
+        # one rank: the result block straight to pinned host memory
+        if host is None:
+            host = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
+        sweep.result_device(host.data_ptr(), stream)
+        ev = torch.cuda.Event()
+        cur = torch.cuda.current_stream(device)
+        ev.record(cur if stream in (None, 0, cur.cuda_stream) else torch.cuda.ExternalStream(stream, device=device))
+        return PendingSweep(sweep, host, ev)
     blk = torch.empty(nbytes, dtype=torch.uint8, device=device)
     sweep.result_device(blk.data_ptr(), stream)
     if world > 1:

@@ -279,7 +279,8 @@ int bote_sweep_create_keys(const bote_planet* p, const uint32_t* servers, uint32
 int bote_sweep_launch(bote_sweep* s, uint64_t rank_begin, uint64_t rank_end, void* hip_stream);
 int bote_sweep_result(bote_sweep* s, void* hip_stream, bote_topk_record* out, uint32_t* out_count,
                       uint64_t* out_valid, uint64_t* out_digest);
-/* Device-side result block for collectives: `dst` (device memory, at least
+/* Device-side result block for collectives: `dst` (device memory, or pinned
+ * host memory for a direct copy to the host; at least
  * bote_sweep_result_bytes()) receives [n_obj x 128 records, ascending, padded
  * with all-ones records][valid u64][digest u64], stream-ordered after the last
  * launch.  Only the first K records of each objective are meaningful. */

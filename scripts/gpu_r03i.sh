@@ -1,0 +1,16 @@
+#!/bin/bash
+# Round 3: full GPU suite + benches (XK binning, one zeroing launch, direct D2H).
+set -u
+mkdir -p gpurun_out
+export PYTHONUNBUFFERED=1
+timeout -k 10 300 python -u __graft_entry__.py > gpurun_out/smoke.log 2>&1
+rc=$?; echo "smoke rc=$rc"; tail -1 gpurun_out/smoke.log; [ $rc -ne 0 ] && exit $rc
+timeout -k 10 900 python -u -m pytest tests/ -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1
+rc=$?; echo "pytest rc=$rc $(tail -1 gpurun_out/gpu_tests.log)"; [ $rc -ne 0 ] && { grep -E "FAIL|Error|assert" gpurun_out/gpu_tests.log | head; exit $rc; }
+for wl in r64n7 r128n6 r128n6_base; do
+  timeout -k 10 300 python -u bench.py --workload $wl --steps 10 --warmup 2 --no-cpu-baseline > gpurun_out/bench_$wl.log 2>&1
+  rc=$?; echo "bench $wl rc=$rc $(grep -o '"ms_per_step": [0-9.]*\|"kernel_ms_avg": [0-9.]*\|"block": [0-9]*\|"lds_bytes": [0-9]*' gpurun_out/bench_$wl.log | tr '\n' ' ')"; [ $rc -ne 0 ] && exit $rc
+done
+BOTE_BENCH_REHEARSAL=1 timeout -k 10 300 python -u bench.py --gpus 2 --steps 5 --warmup 1 --no-cpu-baseline > gpurun_out/rehearsal2.log 2>&1
+rc=$?; echo "rehearsal rc=$rc $(grep -o '"ms_per_step": [0-9.]*' gpurun_out/rehearsal2.log)"
+exit $rc
