@@ -147,8 +147,9 @@ struct bote_sweep {
   // group kernel work chunks per launch range (cached: a bench or a shard
   // re-launches the same range), plus the ticket counter
   struct Chunks {
-    std::vector<uint64_t> host;  // kept alive: the async upload reads it
-    DBuf dev;
+    std::vector<uint64_t> host;   // kept alive: the async upload reads it
+    std::vector<uint64_t> state;  // per chunk: FastArgs::wstate (4 u64)
+    DBuf dev, sdev;
     uint32_t n = 0;
   };
   std::map<std::pair<uint64_t, uint64_t>, std::unique_ptr<Chunks>> chunks;
@@ -992,12 +993,34 @@ static int sweep_chunks(bote_sweep* s, uint64_t rb, uint64_t re, hipStream_t st,
     auto c = std::make_unique<bote_sweep::Chunks>();
     const uint32_t nwaves = s->fgrid * (s->fargs.gbd / 64);
     // (no chunk below ~4 wavefront steps of configs)
-    const uint64_t want = std::min<uint64_t>((uint64_t)nwaves * BOTE_CHUNKS_PER_WAVE, (re - rb) / 256 + 1);
+    const char* cpw_env = getenv("BOTE_CHUNKS_PER_WAVE");  // (A/B timing)
+    const uint64_t cpw = cpw_env ? std::max(1ul, strtoul(cpw_env, nullptr, 0)) : (uint64_t)BOTE_CHUNKS_PER_WAVE;
+    const uint64_t want = std::min<uint64_t>((uint64_t)nwaves * cpw, (re - rb) / 256 + 1);
     if (auto w = walk_for(s, rb, re)) c->host = cut_chunks(*w, rb, re, (uint32_t)want);
     if (!c->host.empty()) {
       c->n = (uint32_t)c->host.size() - 1;
       if (c->dev.alloc(c->host.size() * 8) != hipSuccess) return fail(BOTE_E_NOMEM, "hipMalloc work chunks");
       HIP_TRY(hipMemcpyAsync(c->dev.p, c->host.data(), c->host.size() * 8, hipMemcpyHostToDevice, st));
+      // each chunk's first group (FastArgs::wstate): the kernel starts a
+      // chunk with two loads instead of a device unrank
+      const uint32_t F = s->n - 3;
+      if (F <= 16) {
+        c->state.assign((size_t)c->n * 4, 0);
+        std::vector<uint32_t> p(s->n);
+        for (uint32_t i = 0; i < c->n; ++i) {
+          if (!colex_unrank(c->host[i], s->n, s->ns, p.data())) return fail(BOTE_E_ARG, "chunk rank out of range");
+          uint64_t base = 0, b[2] = {0, 0};
+          for (uint32_t k = 0; k < F; ++k) {
+            base += binom_u64(p[3 + k], k + 4);
+            b[k / 8] |= (uint64_t)p[3 + k] << (8 * (k % 8));
+          }
+          c->state[4 * (size_t)i] = base;
+          c->state[4 * (size_t)i + 1] = b[0];
+          c->state[4 * (size_t)i + 2] = b[1];
+        }
+        if (c->sdev.alloc(c->state.size() * 8) != hipSuccess) return fail(BOTE_E_NOMEM, "hipMalloc chunk states");
+        HIP_TRY(hipMemcpyAsync(c->sdev.p, c->state.data(), c->state.size() * 8, hipMemcpyHostToDevice, st));
+      }
     }
     it = s->chunks.emplace(key, std::move(c)).first;
   }
@@ -1091,9 +1114,12 @@ static int launch_fast_path(bote_sweep* s, uint64_t rb, uint64_t re, hipStream_t
     if (crc) return crc;
     f.nwchunks = ch ? ch->n : 0;
     f.wchunks = ch ? ch->dev.as<uint64_t>() : nullptr;
+    f.wstate = ch && !ch->state.empty() ? ch->sdev.as<uint64_t>() : nullptr;
     if (f.nwchunks) {
-      if (!s->wctr.p && s->wctr.alloc(16) != hipSuccess) return fail(BOTE_E_NOMEM, "hipMalloc work counter");
+      if (!s->wctr.p && s->wctr.alloc(8 * 128) != hipSuccess) return fail(BOTE_E_NOMEM, "hipMalloc work counters");
       f.wctr = s->wctr.as<unsigned int>();
+      // 8 counter shards when the grid divides evenly (equal blocks per shard)
+      f.wshards = s->fgrid % 8 == 0 ? 8u : 1u;
     }
   }
   // counters, deferred count, work tickets, fallback counters: one launch

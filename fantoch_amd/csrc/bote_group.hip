@@ -53,6 +53,11 @@ constexpr int GROUP_MAX_BD = 1024;
 #define BOTE_GROUP_WAVES_PERM 4
 #endif
 // qtab member planes are 1 << a.gqsh bytes apart (>= gbd * 4, a power of two)
+// BOTE_GROUP_BIN_ALL (a build knob, A/B timing): the member-binned client loop
+// of the extended key set on every PERM kernel
+#ifndef BOTE_GROUP_BIN_ALL
+#define BOTE_GROUP_BIN_ALL 0
+#endif
 
 __host__ __device__ constexpr int cmax(int a, int b) { return a > b ? a : b; }
 template <bool B>
@@ -125,7 +130,7 @@ __host__ __device__ inline size_t group_layout(const FastArgs& a, int N, int NLW
   // extended key set (PERM kernels): per wave, N member bins of 64 lanes' u32
   // (the client loop's binned sums, sweep_group_kernel)
   o = (o + 15) & ~(size_t)15;
-  off[14] = o; o += perm && a.keys ? (size_t)(a.gbd / 64) * N * 256 : 0;
+  off[14] = o; o += perm && (a.keys || BOTE_GROUP_BIN_ALL) ? (size_t)(a.gbd / 64) * N * 256 : 0;
   return o;
 }
 
@@ -252,6 +257,12 @@ __device__ __forceinline__ void merge_lists(const T* A, const T* y, T* L) {
 // merges every lane record that beats its objective's K-th record (exact
 // (key, rank) order), updates the thresholds, releases the lock.  The block
 // lists hold exactly K records each (K <= KP).
+// Each output position is a count: a list record's index plus the candidates
+// below it, a candidate's lower bound in the list plus the candidates below it.
+// The candidates stay in their lanes and are read with v_readlane (the loop
+// over them is a chain of scalar reads, not of dependent LDS loads: in the
+// fill phase, 64 candidates per objective, that latency chain held the block's
+// lock for microseconds per merge and was a fixed ~1 ms per launch).
 __device__ __forceinline__ void wave_topk(const TopkLds& t, int* lock, int n_obj, uint32_t K,
                                           const uint64_t (&key)[MAXOBJ], const bool (&ok)[MAXOBJ], uint64_t rank) {
   const uint32_t lane = threadIdx.x & 63;
@@ -261,6 +272,7 @@ __device__ __forceinline__ void wave_topk(const TopkLds& t, int* lock, int n_obj
   }
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  const uint32_t rlo = (uint32_t)rank, rhi = (uint32_t)(rank >> 32);
 #pragma unroll
   for (int o = 0; o < MAXOBJ; ++o) {
     if (o >= n_obj) break;
@@ -270,25 +282,27 @@ __device__ __forceinline__ void wave_topk(const TopkLds& t, int* lock, int n_obj
     const bool p = ok[o] && rec_lt(mine, th);
     const uint64_t m = __ballot(p);
     if (m == 0) continue;
-    const int n = __popcll(m);
-    if (p) t.cand[__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0))] = mine;
-    wave_sync();
-#pragma unroll
-    for (int h = 0; h < KP / 64; ++h) {
-      const int e = lane + 64 * h;
-      if (e < KL) {
-        const Rec x = top[e];
-        int r = e;
-        for (int j = 0; j < n; ++j) r += rec_lt(t.cand[j], x);
-        if (r < KL) t.tmp[r] = x;
-      }
+    // the list records this lane places (e = lane, lane + 64 < K)
+    const bool h0 = (int)lane < KL, h1 = (int)lane + 64 < KL;
+    const Rec x0 = h0 ? top[lane] : rec_max(), x1 = h1 ? top[lane + 64] : rec_max();
+    int r0 = (int)lane, r1 = (int)lane + 64;
+    int rc = p ? lower_bound_rec(top, KL, mine) : 0;
+    const uint32_t klo = (uint32_t)key[o], khi = (uint32_t)(key[o] >> 32);
+    for (uint64_t mm = m; mm; mm &= mm - 1) {
+      const int src = __builtin_ctzll(mm);
+      // (readlane returns int: widen through uint32_t, not by sign extension)
+      const uint64_t ck = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(khi, src) << 32) |
+                          (uint32_t)__builtin_amdgcn_readlane(klo, src);
+      const uint64_t cr = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(rhi, src) << 32) |
+                          (uint32_t)__builtin_amdgcn_readlane(rlo, src);
+      const Rec c = Rec{ck, cr};
+      r0 += rec_lt(c, x0);
+      r1 += rec_lt(c, x1);
+      rc += rec_lt(c, mine);
     }
-    if ((int)lane < n) {
-      const Rec y = t.cand[lane];
-      int r = lower_bound_rec(top, KL, y);
-      for (int j = 0; j < n; ++j) r += rec_lt(t.cand[j], y);
-      if (r < KL) t.tmp[r] = y;
-    }
+    if (h0 && r0 < KL) t.tmp[r0] = x0;
+    if (h1 && r1 < KL) t.tmp[r1] = x1;
+    if (p && rc < KL) t.tmp[rc] = mine;
     wave_sync();
 #pragma unroll
     for (int h = 0; h < KP / 64; ++h)
@@ -368,6 +382,7 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
   constexpr int PV = Pow2<N - 1>::v;                 // variable row: N-1 values, padded
   constexpr int PF = Pow2<F>::v;                     // fixed-to-fixed row: F values (self = INF), padded
   constexpr bool PERM = GC::PERM;
+  constexpr bool BIN = XK || (PERM && BOTE_GROUP_BIN_ALL);  // the member-binned client loop
   static_assert(!XK || (PERM && DEF), "the extended key set runs on the PERM kernels with the default objectives");
   using QT = QTab<N, XK>;
   constexpr int NT = QT::NT;  // leaderless tables (PERM: register byte planes); == NL without XK
@@ -410,8 +425,8 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
   for (uint32_t i = tid; i < (uint32_t)a.n_obj * a.K; i += BD) tk.top[i] = rec_max();
   if (tid < MAXOBJ) tk.thr[tid] = rec_max();
   if (tid == 0) *lock = 0;
-  // XK: the member bins start at zero (each lane re-zeroes its own after use)
-  if constexpr (XK)
+  // BIN: the member bins start at zero (each lane re-zeroes its own after use)
+  if constexpr (BIN)
     for (uint32_t i = tid; i < (BD >> 6) * N * 64; i += BD) ((uint32_t*)(smem + off[14]))[i] = 0;
   __syncthreads();
   const uint32_t cstride = (a.cq_quads + 1) * 8;  // bytes per CQT column
@@ -455,13 +470,22 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
   // configs costs ceil(C(p3, 3) / 64) steps plus its precompute, and the
   // regions of small groups cost up to several times the average.
   bool static_done = false;
+  // The next chunk's ticket is claimed when a chunk starts (its atomic's
+  // latency overlaps the chunk's work), so each wave holds one claimed ticket
+  // ahead; a claimed ticket is always swept by its wave, and every wave ends
+  // on a ticket past the last chunk.
+  const uint32_t wsh = a.wshards ? a.wshards : 1u, wx = blockIdx.x % wsh;
+  unsigned int* const tctr = a.wctr + 32 * wx;  // this block's counter shard
+  uint32_t cnext = 0;
+  if (a.nwchunks && lane == 0) cnext = atomicAdd(tctr, 1u);  // (vector atomic, one lane)
   for (;;) {
   uint64_t r, rend;
+  uint32_t chunk = ~0u;
   if (a.nwchunks) {
-    uint32_t c = 0;
-    if (lane == 0) c = atomicAdd(a.wctr, 1u);  // (vector atomic, one lane)
-    c = uni(c);
+    const uint32_t c = wx + wsh * uni(cnext);
     if (c >= a.nwchunks) break;
+    if (lane == 0) cnext = atomicAdd(tctr, 1u);
+    chunk = c;
     r = uni64(a.wchunks[c]);
     rend = uni64(a.wchunks[c + 1]);
     GASSERT(a, a.rb <= r && r <= rend && rend <= a.re, 0);  // chunk inside the launch range
@@ -478,7 +502,16 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
   if (r < rend) {
     uint32_t hq[F];  // fixed positions p_3 .. p_{N-1} (uniform)
     uint64_t base = 0;
-    {
+    if (a.wstate && chunk != ~0u) {
+      // the chunk's first group, unranked on the host (bote_capi.hip
+      // sweep_chunks): the colex rank of its fixed part, then the positions
+      // as bytes (a device unrank is ~45 dependent binomial loads)
+      const uint64_t* st = a.wstate + 4 * (size_t)chunk;
+      base = uni64(st[0]);
+      const uint64_t b0 = uni64(st[1]), b1 = uni64(st[2]);
+#pragma unroll
+      for (int k = 0; k < F; ++k) hq[k] = (uint32_t)((k < 8 ? b0 >> (8 * k) : b1 >> (8 * (k - 8))) & 0xFFu);
+    } else {
       uint32_t p[N];
       colex_unrank<N>(binom, a.ns, r, p);
 #pragma unroll
@@ -860,7 +893,7 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
 #pragma unroll
             for (int t = 0; t < NT; ++t) {
               const uint32_t w01 = wp[t][0], w2 = wp[t][1], w34 = wp[t][2], w56 = FP >= 2 ? wp[t][FP >= 2 ? 3 : 2] : 0u;
-              if constexpr (!XK) {  // (XK bins the clients by member instead)
+              if constexpr (!BIN) {  // (BIN bins the clients by member instead)
                 QL[t].x = __builtin_amdgcn_perm(w2, w01, 0x0C040200u) | (w34 << 24);
                 QH[t].x = __builtin_amdgcn_perm(w34, __builtin_amdgcn_perm(w2, w01, 0x0C050301u), 0x05020100u);
                 QL[t].y = __builtin_amdgcn_perm(w56, w34, 0x0C060402u);
@@ -1137,8 +1170,8 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
                   flush();
                 }
               };
-              if constexpr (XK) {
-                // ---- XK: the clients binned by nearest member, so the loop
+              if constexpr (BIN) {
+                // ---- BIN: the clients binned by nearest member, so the loop
                 //      does not depend on the number of tables (4 here).  Per
                 //      client one LDS add of (key | 1 << 24) into its member's
                 //      bin (this lane's word of member m at bin + 256 m): the

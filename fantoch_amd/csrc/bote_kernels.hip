@@ -795,8 +795,8 @@ __global__ void zero_ctl_kernel(unsigned long long* counters, unsigned long long
   const uint32_t t = threadIdx.x;
   if (t < 2) counters[t] = 0;
   if (t == 2) *qcount = 0;
-  if (t == 3 && wctr) *wctr = 0;
   if (t >= 4 && t < 6) counters_alt[t - 4] = 0;
+  if (t >= 8 && t < 16 && wctr) wctr[32 * (t - 8)] = 0;  // the 8 ticket-counter shards
 }
 
 hipError_t launch_zero_ctl(unsigned long long* counters, unsigned long long* qcount, unsigned int* wctr,

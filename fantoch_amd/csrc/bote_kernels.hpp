@@ -102,11 +102,18 @@ struct FastArgs {
   uint32_t grx;       // group kernel, n <= 7: per-group position table (1) or per-lane row sorts (0)
   uint32_t keys;      // group kernel: 1 = the extended key set (n = 4..7, default objectives first)
   // group kernel work distribution: nwchunks > 0: waves take cost-balanced
-  // rank chunks [wchunks[c], wchunks[c+1]) from the ticket counter *wctr
-  // (zeroed before each launch); 0: each wave sweeps an equal share of ranks
+  // rank chunks [wchunks[c], wchunks[c+1]) from ticket counters (zeroed
+  // before each launch); 0: each wave sweeps an equal share of ranks.  The
+  // counter is sharded wshards ways (one 128-B line each, wctr[32 * x]):
+  // blocks b with b % wshards == x take chunks x, x + wshards, ... (one
+  // device-scope word saturates near 90 tickets per us, MI355X_MICROARCH.md)
   const uint64_t* wchunks;
   uint32_t nwchunks;
   unsigned int* wctr;
+  uint32_t wshards;
+  // per chunk, 4 u64: the colex rank of its first group's fixed positions,
+  // then those positions as bytes (16 at most); null: unranked on the device
+  const uint64_t* wstate;
   int want_score, p_int;
   int64_t p1i, p2i;  // p_int: min_mean_{fpaxos,epaxos}_improv * nc as integers
   // group kernel mean tests on D = the integer difference of two sums: true
