@@ -153,6 +153,11 @@ struct bote_sweep {
     uint32_t n = 0;
   };
   std::map<std::pair<uint64_t, uint64_t>, std::unique_ptr<Chunks>> chunks;
+  // top-K seed: the sample launch's one-step chunks per launch range (same
+  // layout: starts in host/dev, FastArgs::wstate in state/sdev), its per-chunk
+  // minima and the seed keys
+  std::map<std::pair<uint64_t, uint64_t>, std::unique_ptr<Chunks>> samples;
+  DBuf smin, tseed;
   // host walks of the groups (bote_host.hpp): one walk serves the split and
   // the chunk tables of every sub-range it covers (bote_search_* shares one
   // walk across its shards' sweeps)
@@ -859,6 +864,12 @@ int bote_sweep_create_keys(const bote_planet* p, const uint32_t* servers, uint32
       // workgroups leave LDS for the client lines that 256-thread ones cannot
       // hold (a step has 7.7 distinct (p1, p2) on average at R=64 n=7, 4.0 at
       // R=128 n=6).  pick_group_geometry keeps the best.
+      // the member-binned client loop on the base key set: bench-shaped
+      // sweeps (server identity, digest, F1F2: the SI kernels) with >= 96
+      // clients, where the bin fields cannot overflow
+      f.gbins = !keys && s->def_obj && bote::group_uses_lines(n) && nc >= 96 && nc < 256 && f.srv_identity &&
+                f.want_digest && f.ft_metric == 2 && (uint64_t)nc * (16ull * maxlat + 15) < (1ull << 24) &&
+                2 * (16ull * maxlat + 15) * (16ull * maxlat + 15) < (1ull << 32);
       struct GGeo {
         uint32_t bd = 0, grx = 0, gslots = 0, gqsh = 10;
         int occ = 0;
@@ -1099,6 +1110,64 @@ static int launch_generic(bote_sweep* s, uint64_t rb, uint64_t re, hipStream_t s
   return merge_chain(s, s->grid, st);
 }
 
+// The top-K seed of a group launch over [rb, re) (launch_fast_path): sets
+// f.tseed, or leaves it null when the range is too small to sample.
+static int sample_seed(bote_sweep* s, bote::FastArgs& f, uint64_t rb, uint64_t re, hipStream_t st) {
+  const uint32_t nwaves = s->fgrid * (s->fargs.gbd / 64);
+  const uint32_t nsamp = std::min<uint32_t>(4096, nwaves);
+  // samples are disjoint one-step chunks and at most 1/8 of the range
+  if (nsamp < s->K || re - rb < (uint64_t)nsamp * 64 * 8) return BOTE_OK;
+  auto key = std::make_pair(rb, re);
+  auto it = s->samples.find(key);
+  if (it == s->samples.end()) {
+    if (s->samples.size() >= 16) {
+      if (s->last_stream) HIP_TRY(hipStreamSynchronize(s->last_stream));
+      HIP_TRY(hipStreamSynchronize(st));
+      s->samples.clear();
+    }
+    auto c = std::make_unique<bote_sweep::Chunks>();
+    c->n = nsamp;
+    c->host.resize(nsamp);
+    c->state.assign((size_t)nsamp * 4, 0);
+    std::vector<uint32_t> p(s->n);
+    const uint32_t F = s->n - 3;
+    if (F > 16) return BOTE_OK;
+    for (uint32_t i = 0; i < nsamp; ++i) {
+      const uint64_t b = rb + (uint64_t)(((unsigned __int128)(re - rb - 64) * i) / nsamp);
+      c->host[i] = b;
+      if (!colex_unrank(b, s->n, s->ns, p.data())) return fail(BOTE_E_ARG, "sample rank out of range");
+      uint64_t base = 0, w[2] = {0, 0};
+      for (uint32_t k = 0; k < F; ++k) {
+        base += binom_u64(p[3 + k], k + 4);
+        w[k / 8] |= (uint64_t)p[3 + k] << (8 * (k % 8));
+      }
+      c->state[4 * (size_t)i] = base;
+      c->state[4 * (size_t)i + 1] = w[0];
+      c->state[4 * (size_t)i + 2] = w[1];
+    }
+    if (c->dev.alloc(c->host.size() * 8) != hipSuccess || c->sdev.alloc(c->state.size() * 8) != hipSuccess)
+      return fail(BOTE_E_NOMEM, "hipMalloc sample chunks");
+    HIP_TRY(hipMemcpyAsync(c->dev.p, c->host.data(), c->host.size() * 8, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(c->sdev.p, c->state.data(), c->state.size() * 8, hipMemcpyHostToDevice, st));
+    it = s->samples.emplace(key, std::move(c)).first;
+  }
+  const bote_sweep::Chunks* c = it->second.get();
+  if (s->smin.reserve((size_t)s->n_obj * nsamp * 8) != hipSuccess || s->tseed.reserve(bote::MAXOBJ * 8) != hipSuccess)
+    return fail(BOTE_E_NOMEM, "hipMalloc top-K seed");
+  HIP_TRY(hipMemsetAsync(s->smin.p, 0xFF, (size_t)s->n_obj * nsamp * 8, st));
+  bote::FastArgs fs = f;
+  fs.smin = s->smin.as<uint64_t>();
+  fs.tseed = nullptr;
+  fs.wchunks = c->dev.as<uint64_t>();
+  fs.wstate = c->sdev.as<uint64_t>();
+  fs.nwchunks = nsamp;
+  fs.wctr = f.wctr + 256;  // the sample launch's ticket shards
+  HIP_TRY(bote::launch_group(fs, s->n, s->def_obj, s->fgrid, s->fshm, st));
+  HIP_TRY(bote::launch_seed(fs.smin, nsamp, s->n_obj, s->K, s->tseed.as<uint64_t>(), st));
+  f.tseed = s->tseed.as<uint64_t>();
+  return BOTE_OK;
+}
+
 // Fast kernel over [rb, re), then the generic kernel over its deferred ranks.
 static int launch_fast_path(bote_sweep* s, uint64_t rb, uint64_t re, hipStream_t st) {
   bote::FastArgs f = s->fargs;
@@ -1116,7 +1185,8 @@ static int launch_fast_path(bote_sweep* s, uint64_t rb, uint64_t re, hipStream_t
     f.wchunks = ch ? ch->dev.as<uint64_t>() : nullptr;
     f.wstate = ch && !ch->state.empty() ? ch->sdev.as<uint64_t>() : nullptr;
     if (f.nwchunks) {
-      if (!s->wctr.p && s->wctr.alloc(8 * 128) != hipSuccess) return fail(BOTE_E_NOMEM, "hipMalloc work counters");
+      // (8 shards of 128 B for the main launch, 8 for the sample launch)
+      if (!s->wctr.p && s->wctr.alloc(16 * 128) != hipSuccess) return fail(BOTE_E_NOMEM, "hipMalloc work counters");
       f.wctr = s->wctr.as<unsigned int>();
       // 8 counter shards when the grid divides evenly (equal blocks per shard)
       f.wshards = s->fgrid % 8 == 0 ? 8u : 1u;
@@ -1125,6 +1195,16 @@ static int launch_fast_path(bote_sweep* s, uint64_t rb, uint64_t re, hipStream_t
   // counters, deferred count, work tickets, fallback counters: one launch
   HIP_TRY(bote::launch_zero_ctl(s->counters.as<unsigned long long>(), s->qcount.as<unsigned long long>(),
                                 f.nwchunks ? f.wctr : nullptr, s->counters_alt.as<unsigned long long>(), st));
+  // top-K seed: one step of 64 configs per wave at evenly spaced ranks, then
+  // per objective the K-th least of the chunks' minimum keys (a bound on the
+  // range's K-th key: K distinct configs of the range reach it), so that the
+  // blocks' lists start with a threshold instead of filling from empty (the
+  // fill costs about the same per block whatever the range: at 1/8 of R=64
+  // n=7 it was 1/8 of the kernel)
+  if (s->group && f.nwchunks && s->n_obj && s->K) {
+    int src = sample_seed(s, f, rb, re, st);
+    if (src) return src;
+  }
   hipEvent_t *e0 = nullptr, *e1 = nullptr;
   int rc;
   if ((rc = timing_slot(s, e0, e1))) return rc;

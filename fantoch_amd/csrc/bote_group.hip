@@ -130,7 +130,7 @@ __host__ __device__ inline size_t group_layout(const FastArgs& a, int N, int NLW
   // extended key set (PERM kernels): per wave, N member bins of 64 lanes' u32
   // (the client loop's binned sums, sweep_group_kernel)
   o = (o + 15) & ~(size_t)15;
-  off[14] = o; o += perm && (a.keys || BOTE_GROUP_BIN_ALL) ? (size_t)(a.gbd / 64) * N * 256 : 0;
+  off[14] = o; o += perm && (a.keys || a.gbins || BOTE_GROUP_BIN_ALL) ? (size_t)(a.gbd / 64) * N * 256 : 0;
   return o;
 }
 
@@ -277,9 +277,9 @@ __device__ __forceinline__ void wave_topk(const TopkLds& t, int* lock, int n_obj
   for (int o = 0; o < MAXOBJ; ++o) {
     if (o >= n_obj) break;
     Rec* top = t.top + o * KL;
-    const Rec th = top[KL - 1];
     const Rec mine = Rec{key[o], rank};
-    const bool p = ok[o] && rec_lt(mine, th);
+    // thr: the lesser of the list's K-th record and the seed (never above it)
+    const bool p = ok[o] && rec_lt(mine, t.thr[o]);
     const uint64_t m = __ballot(p);
     if (m == 0) continue;
     // the list records this lane places (e = lane, lane + 64 < K)
@@ -308,7 +308,7 @@ __device__ __forceinline__ void wave_topk(const TopkLds& t, int* lock, int n_obj
     for (int h = 0; h < KP / 64; ++h)
       if ((int)lane + 64 * h < KL) top[lane + 64 * h] = t.tmp[lane + 64 * h];
     wave_sync();
-    if (lane == 0) t.thr[o] = top[K - 1];
+    if (lane == 0 && rec_lt(top[K - 1], t.thr[o])) t.thr[o] = top[K - 1];
     wave_sync();
   }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
@@ -365,7 +365,10 @@ constexpr uint32_t GROUP_XK_MAX_BD = 768;
 #ifndef BOTE_GROUP_UNROLL
 #define BOTE_GROUP_UNROLL 4
 #endif
-template <int N, bool DEF, bool SI, bool RXC, bool XK>
+// BN: the base key set with the member-binned client loop (the extended key
+// set's, below); the host picks it for bench-shaped sweeps with >= 96 clients
+// (FastArgs::gbins: R=128 n=6 179.8 -> 168.2 ms; neutral at 64 clients)
+template <int N, bool DEF, bool SI, bool RXC, bool XK, bool BN = false>
 __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
                                   XK ? BOTE_GROUP_WAVES_XK : (GCfg<N>::PERM ? BOTE_GROUP_WAVES_PERM : BOTE_GROUP_WAVES))
     sweep_group_kernel(FastArgs a) {
@@ -382,7 +385,7 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
   constexpr int PV = Pow2<N - 1>::v;                 // variable row: N-1 values, padded
   constexpr int PF = Pow2<F>::v;                     // fixed-to-fixed row: F values (self = INF), padded
   constexpr bool PERM = GC::PERM;
-  constexpr bool BIN = XK || (PERM && BOTE_GROUP_BIN_ALL);  // the member-binned client loop
+  constexpr bool BIN = XK || (PERM && (BN || BOTE_GROUP_BIN_ALL));  // the member-binned client loop
   static_assert(!XK || (PERM && DEF), "the extended key set runs on the PERM kernels with the default objectives");
   using QT = QTab<N, XK>;
   constexpr int NT = QT::NT;  // leaderless tables (PERM: register byte planes); == NL without XK
@@ -423,7 +426,9 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
   }
   for (uint32_t i = tid; i < a.ns; i += BD) srv[i] = a.srv[i];
   for (uint32_t i = tid; i < (uint32_t)a.n_obj * a.K; i += BD) tk.top[i] = rec_max();
-  if (tid < MAXOBJ) tk.thr[tid] = rec_max();
+  // thresholds start at the seed keys (FastArgs::tseed: a bound on each
+  // objective's K-th key over the launch range, from the sample launch)
+  if (tid < MAXOBJ) tk.thr[tid] = a.tseed && tid < a.n_obj ? Rec{a.tseed[tid], ~0ull} : rec_max();
   if (tid == 0) *lock = 0;
   // BIN: the member bins start at zero (each lane re-zeroes its own after use)
   if constexpr (BIN)
@@ -487,7 +492,7 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
     if (lane == 0) cnext = atomicAdd(tctr, 1u);
     chunk = c;
     r = uni64(a.wchunks[c]);
-    rend = uni64(a.wchunks[c + 1]);
+    rend = a.smin ? min(r + 64, a.re) : uni64(a.wchunks[c + 1]);  // (sample chunks: one step each)
     GASSERT(a, a.rb <= r && r <= rend && rend <= a.re, 0);  // chunk inside the launch range
   } else {
     if (static_done) break;
@@ -979,7 +984,7 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
           }
           GASSERT(a, bi < (uint32_t)N, 7);  // leader member
           if (amb) {
-            defer_rank(a, rank);
+            if (!a.smin) defer_rank(a, rank);
             have = false;
           }
           if (have) {
@@ -1417,7 +1422,7 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
                 }
               }
               if (defer) {
-                defer_rank(a, rank);
+                if (!a.smin) defer_rank(a, rank);
               } else {
                 if (valid) ++valid_cnt;
                 if ((SI || a.want_digest) && !ABLATE(a, 16)) {
@@ -1491,13 +1496,28 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
                 }
               }
             } else {
-              if (!finish_config<N>(a, mom, vlead, bi, rank, tk.thr, pnc1, pnc2, valid_cnt, digest, key, ok))
+              if (!finish_config<N>(a, mom, vlead, bi, rank, tk.thr, pnc1, pnc2, valid_cnt, digest, key, ok) && !a.smin)
                 defer_rank(a, rank);
             }
           }
         }
         // ---- top-K: lock-free screen, exact merge under the block lock
-        if (!ABLATE(a, 4)) {
+        if (a.smin) {
+          // sample launch: per objective the least key of this chunk's configs
+          const int nobj = XK ? 8 : (DEF ? 5 : a.n_obj);
+#pragma unroll
+          for (int o = 0; o < MAXOBJ; ++o) {
+            if (o >= nobj) break;
+            uint64_t v = ok[o] ? key[o] : ~0ull;
+#pragma unroll
+            for (int d = 32; d >= 1; d >>= 1) {
+              const uint64_t w = ((uint64_t)(uint32_t)__shfl_xor((int)(v >> 32), d) << 32) |
+                                 (uint32_t)__shfl_xor((int)(uint32_t)v, d);
+              v = w < v ? w : v;
+            }
+            if (lane == 0 && v != ~0ull) atomicMin((unsigned long long*)&a.smin[(size_t)o * a.nwchunks + chunk], v);
+          }
+        } else if (!ABLATE(a, 4)) {
           const int nobj = XK ? 8 : (DEF ? 5 : a.n_obj);
           bool pass = false;
 #pragma unroll
@@ -1532,6 +1552,7 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
   }
   wave_sync();  // (the next chunk rewrites the group line)
   }
+  if (a.smin) return;  // (the sample launch: no counters, no lists; no barrier follows)
   if (valid_cnt) atomicAdd(&a.out_counters[0], (unsigned long long)valid_cnt);
   if (digest) atomicAdd(&a.out_counters[1], (unsigned long long)digest);
   __syncthreads();
@@ -1543,9 +1564,9 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
 }
 
 // ------------------------------------------------------------- launcher ---
-template <int N, bool DEF, bool SI, bool RXC, bool XK>
+template <int N, bool DEF, bool SI, bool RXC, bool XK, bool BN = false>
 static hipError_t launch_group_n(const FastArgs& a, uint32_t grid, size_t shm, hipStream_t st) {
-  auto k = sweep_group_kernel<N, DEF, SI, RXC, XK>;
+  auto k = sweep_group_kernel<N, DEF, SI, RXC, XK, BN>;
   hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k, dim3(grid), dim3(a.gbd), shm, st, a);
@@ -1566,6 +1587,9 @@ static const void* group_fn_n(const FastArgs& a, bool def) {
                                 : (const void*)sweep_group_kernel<N, true, true, false, true>)
                        : (const void*)sweep_group_kernel<N, true, false, false, true>;
   } else {
+    if (def && group_si(a) && a.gbins)
+      return a.grx ? (const void*)sweep_group_kernel<N, true, true, true, false, true>
+                   : (const void*)sweep_group_kernel<N, true, true, false, false, true>;
     return def ? (group_si(a) ? (a.grx ? (const void*)sweep_group_kernel<N, true, true, true, false>
                                        : (const void*)sweep_group_kernel<N, true, true, false, false>)
                               : (const void*)sweep_group_kernel<N, true, false, false, false>)
@@ -1580,6 +1604,9 @@ static hipError_t launch_group_x(const FastArgs& a, bool def, uint32_t grid, siz
                                 : launch_group_n<N, true, true, false, true>(a, grid, shm, st))
                        : launch_group_n<N, true, false, false, true>(a, grid, shm, st);
   } else {
+    if (def && group_si(a) && a.gbins)
+      return a.grx ? launch_group_n<N, true, true, true, false, true>(a, grid, shm, st)
+                   : launch_group_n<N, true, true, false, false, true>(a, grid, shm, st);
     return def ? (group_si(a) ? (a.grx ? launch_group_n<N, true, true, true, false>(a, grid, shm, st)
                                        : launch_group_n<N, true, true, false, false>(a, grid, shm, st))
                               : launch_group_n<N, true, false, false, false>(a, grid, shm, st))

@@ -796,12 +796,47 @@ __global__ void zero_ctl_kernel(unsigned long long* counters, unsigned long long
   if (t < 2) counters[t] = 0;
   if (t == 2) *qcount = 0;
   if (t >= 4 && t < 6) counters_alt[t - 4] = 0;
-  if (t >= 8 && t < 16 && wctr) wctr[32 * (t - 8)] = 0;  // the 8 ticket-counter shards
+  if (t >= 8 && t < 24 && wctr) wctr[32 * (t - 8)] = 0;  // the 8 ticket-counter shards, main and sample launch
 }
 
 hipError_t launch_zero_ctl(unsigned long long* counters, unsigned long long* qcount, unsigned int* wctr,
                            unsigned long long* counters_alt, hipStream_t st) {
   hipLaunchKernelGGL(zero_ctl_kernel, dim3(1), dim3(64), 0, st, counters, qcount, wctr, counters_alt);
+  return hipGetLastError();
+}
+
+// The top-K seed: per objective (one block each) the K-th least of the
+// sample launch's per-chunk minima (a bitonic sort of <= 4096 keys in LDS);
+// all-ones (no bound) when fewer than K samples have the objective.
+__global__ void __launch_bounds__(1024) seed_kernel(const uint64_t* smin, uint32_t nsamp, uint32_t K, uint64_t* tseed) {
+  __shared__ uint64_t v[4096];
+  const uint32_t o = blockIdx.x, tid = threadIdx.x;
+  uint32_t P = 1;
+  while (P < nsamp) P <<= 1;
+  for (uint32_t i = tid; i < P; i += blockDim.x) v[i] = i < nsamp ? smin[(size_t)o * nsamp + i] : ~0ull;
+  __syncthreads();
+  for (uint32_t k = 2; k <= P; k <<= 1) {
+    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+      for (uint32_t i = tid; i < P; i += blockDim.x) {
+        const uint32_t l = i ^ j;
+        if (l > i) {
+          const uint64_t a = v[i], b = v[l];
+          if (((i & k) == 0) == (a > b)) {
+            v[i] = b;
+            v[l] = a;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  if (tid == 0) tseed[o] = nsamp >= K && K > 0 ? v[K - 1] : ~0ull;
+}
+
+hipError_t launch_seed(const uint64_t* smin, uint32_t nsamp, uint32_t n_obj, uint32_t K, uint64_t* tseed,
+                       hipStream_t st) {
+  if (nsamp > 4096) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(seed_kernel, dim3(n_obj), dim3(1024), 0, st, smin, nsamp, K, tseed);
   return hipGetLastError();
 }
 

@@ -101,6 +101,7 @@ struct FastArgs {
   uint32_t gslots;    // group kernel, n <= 7: client lines per wave (0: none), see bote_group.hip
   uint32_t grx;       // group kernel, n <= 7: per-group position table (1) or per-lane row sorts (0)
   uint32_t keys;      // group kernel: 1 = the extended key set (n = 4..7, default objectives first)
+  uint32_t gbins;     // group kernel, base key set: the member-binned client loop (bote_group.hip BN)
   // group kernel work distribution: nwchunks > 0: waves take cost-balanced
   // rank chunks [wchunks[c], wchunks[c+1]) from ticket counters (zeroed
   // before each launch); 0: each wave sweeps an equal share of ranks.  The
@@ -114,6 +115,14 @@ struct FastArgs {
   // per chunk, 4 u64: the colex rank of its first group's fixed positions,
   // then those positions as bytes (16 at most); null: unranked on the device
   const uint64_t* wstate;
+  // top-K seed (bote_capi.hip launch_fast_path): the sample launch (smin
+  // non-null) takes nwchunks one-step chunks at wchunks[c] and records, per
+  // objective o, the least key of chunk c at smin[o * nwchunks + c] (no lists,
+  // counters or deferrals); seed_kernel turns those into tseed[o], the K-th
+  // least, a bound on the launch's K-th key that the main launch starts its
+  // thresholds at
+  uint64_t* smin;
+  const uint64_t* tseed;
   int want_score, p_int;
   int64_t p1i, p2i;  // p_int: min_mean_{fpaxos,epaxos}_improv * nc as integers
   // group kernel mean tests on D = the integer difference of two sums: true
@@ -193,6 +202,8 @@ hipError_t launch_merge_sel(const Rec* src, uint32_t n_lists, const Rec* alt, ui
 // dst[0..1] = (*sel > cap ? alt : src)[0..1]
 hipError_t launch_zero_ctl(unsigned long long* counters, unsigned long long* qcount, unsigned int* wctr,
                            unsigned long long* counters_alt, hipStream_t st);
+hipError_t launch_seed(const uint64_t* smin, uint32_t nsamp, uint32_t n_obj, uint32_t K, uint64_t* tseed,
+                       hipStream_t st);
 hipError_t launch_pick_counters(const unsigned long long* src, const unsigned long long* alt,
                                 const unsigned long long* sel, uint64_t cap, uint64_t* dst, hipStream_t st);
 
