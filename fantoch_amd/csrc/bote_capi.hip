@@ -790,6 +790,11 @@ int bote_sweep_create_keys(const bote_planet* p, const uint32_t* servers, uint32
     // per dot2 into 32 bits (keys32 below requires 2 key^2 < 2^32)
     const uint64_t kmax = 16ull * maxlat + 15, kq = 4 * kmax * kmax;
     f.k_flush = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(1u << 20, 0xFFFFFFFFull / kq));
+    // every slot's sum of squares below 2^32 (a value is at most a latency
+    // plus a quorum latency, 2 max, over nc >= N clients): the bench-shaped
+    // group kernels keep the moments in 32 bits (bote_group.hip S32)
+    f.s32 = (uint64_t)std::max(nc, n) * amax * amax < (1ull << 32) ? 1u : 0u;
+    f.v32 = f.s32 && (uint64_t)std::max(nc, n) * std::max(nc, n) * amax * amax < (1ull << 32) ? 1u : 0u;
     f.want_score = a.want_score;
     f.p_fmean = a.p_fmean;
     f.p_emean = a.p_emean;
@@ -1005,7 +1010,8 @@ static int sweep_chunks(bote_sweep* s, uint64_t rb, uint64_t re, hipStream_t st,
     const uint32_t nwaves = s->fgrid * (s->fargs.gbd / 64);
     // (no chunk below ~4 wavefront steps of configs)
     const char* cpw_env = getenv("BOTE_CHUNKS_PER_WAVE");  // (A/B timing)
-    const uint64_t cpw = cpw_env ? std::max(1ul, strtoul(cpw_env, nullptr, 0)) : (uint64_t)BOTE_CHUNKS_PER_WAVE;
+    const uint64_t cpw = cpw_env ? std::max(1ul, strtoul(cpw_env, nullptr, 0))
+                                 : (uint64_t)chunks_per_wave(re - rb, nwaves, s->fargs.nc, BOTE_CHUNKS_PER_WAVE);
     const uint64_t want = std::min<uint64_t>((uint64_t)nwaves * cpw, (re - rb) / 256 + 1);
     if (auto w = walk_for(s, rb, re)) c->host = cut_chunks(*w, rb, re, (uint32_t)want);
     if (!c->host.empty()) {

@@ -373,6 +373,10 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
                                   XK ? BOTE_GROUP_WAVES_XK : (GCfg<N>::PERM ? BOTE_GROUP_WAVES_PERM : BOTE_GROUP_WAVES))
     sweep_group_kernel(FastArgs a) {
   const bool sid = SI || a.srv_identity;
+  // S32 (the SI kernels; the host admits them only where FastArgs::s32
+  // holds): every slot's sum of squares fits 32 bits, so the moments, the
+  // leader columns' sums of squares and the digest folds stay 32-bit
+  constexpr bool S32 = SI;
   // the position table: a launch argument, compiled in (RXC) on SI kernels
   const bool use_rx = GCfg<N>::RX && (SI ? RXC : a.grx != 0);
   using QC = QCfg<N>;
@@ -608,15 +612,17 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
       // ---------------- the group's configs, 64 per step
       const uint64_t cend = uni64(gend < rend ? gend : rend);
       GASSERT(a, low + (cend - r) <= a.lowtab_n, 2);  // low-table rows of the group's configs
-      uint32_t lp3 = a.lowtab[low + min((uint64_t)lane, cend - r - 1)];  // prefetched
-      while (r < cend) {
-        const uint32_t len = (uint32_t)min((uint64_t)64, cend - r);
+      // the step loop counts in 32 bits (a group holds C(p3, 3) < 2^32
+      // configs, and the low table's rows are indexed in 32 bits), so its
+      // control stays on the scalar unit (there is no 64-bit scalar compare)
+      uint32_t left = uni((uint32_t)(cend - r)), lo32 = uni((uint32_t)low);
+      uint32_t lp3 = a.lowtab[lo32 + min(lane, left - 1)];  // prefetched
+      while (left) {
+        const uint32_t len = min(64u, left);
         bool have = lane < len;
         const uint32_t cur = lp3;
-        {  // prefetch the next step's low part (the load overlaps this step)
-          const uint64_t nr = r + len;
-          if (nr < cend) lp3 = a.lowtab[low + len + min((uint64_t)lane, cend - nr - 1)];
-        }
+        // prefetch the next step's low part (the load overlaps this step)
+        if (left > len) lp3 = a.lowtab[lo32 + len + min(lane, left - len - 1)];
         uint64_t key[MAXOBJ];
         bool ok[MAXOBJ];
 #pragma unroll
@@ -680,7 +686,7 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
           for (int i = 0; i < 3; ++i) rv[i] = sid ? pv[i] : srv[pv[i]];
           uint32_t cv[3];  // RQT column of each variable member
 #pragma unroll
-          for (int i = 0; i < 3; ++i) cv[i] = rqt + rv[i] * rstride;
+          for (int i = 0; i < 3; ++i) cv[i] = __umul24(rv[i], rstride) + rqt;  // (one v_mad_u32_u24)
           // member m: 0..2 variable, 3.. fixed (config order = ascending positions)
           uint32_t Q2[N], Q3[N];
           uint32_t cS1p = 0, cS1e = 0;  // colocated sums: packed (t0 | t1 << 16), third table
@@ -1062,7 +1068,8 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
                 s2[t] = 0;
                 p1[t] = 0;
               }
-              const uint32_t c0 = cqt + rv[0] * cstride, c1 = cqt + rv[1] * cstride, c2 = cqt + rv[2] * cstride;
+              const uint32_t c0 = __umul24(rv[0], cstride) + cqt, c1 = __umul24(rv[1], cstride) + cqt,
+                             c2 = __umul24(rv[2], cstride) + cqt;
               // (m << qsh) + qlane in one instruction (the compiler would
               // otherwise re-associate it into shift, and, add)
               auto qaddr = [&](uint32_t m) {
@@ -1139,7 +1146,7 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
               auto flush = [&]() {
 #pragma unroll
                 for (int t = 0; t < NT; ++t) {
-                  S2[t] += s2[t];
+                  S2[t] = S32 ? (uint64_t)((uint32_t)S2[t] + s2[t]) : S2[t] + s2[t];
                   s2[t] = 0;
                   S1[t] += (p1[t] & 0xFFFFu) + (p1[t] >> 16);
                   p1[t] = 0;
@@ -1301,6 +1308,7 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
                   }
                   S1[t] = s1;
                   S2[t] = L2 + ((uint64_t)x << 1) + qq;
+                  if constexpr (S32) S2[t] = (uint32_t)S2[t];  // (< 2^32: FastArgs::s32)
                 }
               } else {
                 if (PERM && use_lines) clients(BoolC<PERM>{});
@@ -1329,13 +1337,21 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
             }
             // ---- Input FPaxos from the leader column's sums
             const uint32_t lc1 = lrec[lpos].x;
-            const uint64_t lc2 = cs2[lpos];
-            mom[SLOT_FF1] = leader_mom(lc1, lc2, nc, lq2);
-            mom[SLOT_FF2] = leader_mom(lc1, lc2, nc, lq3);
+            if constexpr (S32) {
+              // sum (L + q) and sum (L + q)^2 = c2 + q (c1 + S1), in 32 bits
+              const uint32_t lc2 = (uint32_t)cs2[lpos];
+              const uint32_t m2 = __umul24(nc, lq2) + lc1, m3 = __umul24(nc, lq3) + lc1;
+              mom[SLOT_FF1] = Mom{m2, (uint32_t)(lq2 * (lc1 + m2) + lc2), nc};
+              mom[SLOT_FF2] = Mom{m3, (uint32_t)(lq3 * (lc1 + m3) + lc2), nc};
+            } else {
+              const uint64_t lc2 = cs2[lpos];
+              mom[SLOT_FF1] = leader_mom(lc1, lc2, nc, lq2);
+              mom[SLOT_FF2] = leader_mom(lc1, lc2, nc, lq3);
+            }
             // ---- Colocated: FPaxos reads the leader's column of the config
             //      submatrix; leaderless values are the members' own quorums
             {
-              const uint32_t lcol = rqt + lreg * rstride;
+              const uint32_t lcol = __umul24(lreg, rstride) + rqt;
               // sum_k (v_k + q) and sum_k (v_k + q)^2 from sum v and sum v^2
               uint32_t sv = 0, sv2 = 0;
 #pragma unroll
@@ -1370,8 +1386,21 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
               const uint32_t s1 = (uint32_t)m.s1;
               return (uint64_t)m.cnt * m.s2 - (uint64_t)s1 * s1;
             };
-            const uint64_t Va1 = mom_v32(mom[SLOT_AF1]);
-            const float va1 = u64_to_f32(Va1);
+            // V and its f32 value; with FastArgs::v32 (S32 kernels) every
+            // V = cnt s2 - s1^2 < cnt s2 fits 32 bits
+            auto vmom = [&](const Mom& m, uint64_t& V, float& vf) {
+              if (S32 && a.v32) {
+                const uint32_t v = m.cnt * (uint32_t)m.s2 - (uint32_t)m.s1 * (uint32_t)m.s1;
+                V = v;
+                vf = (float)v;
+              } else {
+                V = mom_v32(m);
+                vf = u64_to_f32(V);
+              }
+            };
+            uint64_t Va1;
+            float va1;
+            vmom(mom[SLOT_AF1], Va1, va1);
             if constexpr (DEF) {
               // ---- compute_score validity (search.rs:421-472), exact.  The
               //      integer mean tests of every f first; the COV tests only
@@ -1409,9 +1438,10 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
                     if (f > fcap) break;
                     const Mom& ma = mom[f == 1 ? SLOT_AF1 : SLOT_AF2];
                     const Mom& mf = mom[f == 1 ? SLOT_FF1 : SLOT_FF2];
-                    const uint64_t Va = f == 1 ? Va1 : mom_v32(ma);
+                    uint64_t Va = Va1;
+                    float vaf = va1;
+                    if (f != 1) vmom(ma, Va, vaf);
                     if (vlead == 0.0 && Va == 0) continue;  // both COV 0
-                    const float vaf = f == 1 ? va1 : u64_to_f32(Va);
                     const int c = cov2_sign(vlead32, (uint32_t)mf.s1, vaf, (uint32_t)ma.s1, [&] { return vlead; },
                                             [&] { return (double)Va; });
                     lt = lt || c < 0;
@@ -1526,9 +1556,13 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
           if (__ballot(pass)) wave_topk(tk, lock, nobj, a.K, key, ok, rank);
         }
         r += len;
-        low += len;
+        lo32 += len;
+        left -= len;
       }
-      if (r >= rend) break;
+      // (a sample chunk stops at its first group's end: any subset of the
+      // range bounds its K-th key, and a sample across many small groups,
+      // as at rank 0, cost one precompute each: the launch's slowest wave)
+      if (r >= rend || a.smin) break;
       // ---------------- next group: colex successor of the fixed positions
       // (a combination of {3 .. ns-1}; the smallest fixed position is >= 3)
       {
@@ -1575,7 +1609,7 @@ static hipError_t launch_group_n(const FastArgs& a, uint32_t grid, size_t shm, h
 
 // The instantiation launch_group runs for these arguments (its occupancy
 // decides the persistent grid, so it must be the kernel that runs).
-static bool group_si(const FastArgs& a) { return a.srv_identity && a.want_digest && a.ft_metric == 2; }
+static bool group_si(const FastArgs& a) { return a.srv_identity && a.want_digest && a.ft_metric == 2 && a.s32; }
 
 // the extended key set: PERM kernels (n = 4..7) with the default objectives
 bool group_supports_keys(uint32_t n, uint32_t bd) { return n >= 4 && n <= 7 && group_uses_lines(n) && bd <= GROUP_XK_MAX_BD; }
@@ -1618,8 +1652,12 @@ static const void* group_fn(const FastArgs& a, uint32_t n, bool def) {
   switch (n) {
 #define FN_CASE(NN) case NN: return a.keys ? group_fn_n<NN, true>(a, def) : group_fn_n<NN, false>(a, def);
 #define FN_CASE0(NN) case NN: return a.keys ? nullptr : group_fn_n<NN, false>(a, def);
+#ifdef BOTE_ISA_N7
+    FN_CASE(7)
+#else
     FN_CASE(4) FN_CASE(5) FN_CASE(6) FN_CASE(7) FN_CASE0(8) FN_CASE0(9) FN_CASE0(10) FN_CASE0(11) FN_CASE0(12)
     FN_CASE0(13) FN_CASE0(14) FN_CASE0(15) FN_CASE0(16)
+#endif
 #undef FN_CASE
 #undef FN_CASE0
     default: return nullptr;
@@ -1641,8 +1679,12 @@ hipError_t launch_group(const FastArgs& a, uint32_t n, bool def, uint32_t grid, 
   case NN: return a.keys ? launch_group_x<NN, true>(a, def, grid, shm, st) : launch_group_x<NN, false>(a, def, grid, shm, st);
 #define GS_CASE0(NN) \
   case NN: return a.keys ? hipErrorInvalidValue : launch_group_x<NN, false>(a, def, grid, shm, st);
+#ifdef BOTE_ISA_N7  // (analysis builds only: the n = 7 kernels, for assembly listings)
+    GS_CASE(7)
+#else
     GS_CASE(4) GS_CASE(5) GS_CASE(6) GS_CASE(7) GS_CASE0(8) GS_CASE0(9) GS_CASE0(10) GS_CASE0(11) GS_CASE0(12)
     GS_CASE0(13) GS_CASE0(14) GS_CASE0(15) GS_CASE0(16)
+#endif
 #undef GS_CASE
 #undef GS_CASE0
     default: return hipErrorInvalidValue;

@@ -71,6 +71,14 @@ double group_cost(uint32_t nc) {
   return std::min(8.0, std::max(0.25, c));
 }
 
+uint32_t chunks_per_wave(uint64_t ranks, uint32_t nwaves, uint32_t nc, uint32_t cap) {
+  const uint32_t lo = std::min<uint32_t>(4, cap);
+  if (nwaves == 0) return lo;
+  const double T = (double)ranks / 64.0 / (double)nwaves;
+  const double c = std::sqrt(T / group_cost(nc));
+  return (uint32_t)std::max<double>(lo, std::min<double>(cap, std::floor(c + 0.5)));
+}
+
 std::shared_ptr<GroupWalk> walk_groups(uint32_t ns, uint32_t n, uint32_t nc, uint64_t rb, uint64_t re,
                                        uint64_t max_groups) {
   if (re <= rb || n < 4 || n > ns) return nullptr;

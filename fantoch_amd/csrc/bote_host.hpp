@@ -48,6 +48,13 @@ std::shared_ptr<GroupWalk> walk_groups(uint32_t ns, uint32_t n, uint32_t nc, uin
 // walk's range) into parts of equal estimated cost; empty if the walk does not
 // cover [b, e).
 std::vector<uint64_t> cut_chunks(const GroupWalk& w, uint64_t b, uint64_t e, uint32_t nchunks);
+// Work chunks per wavefront for a launch of `ranks` configs on `nwaves`
+// waves with nc clients: every chunk re-runs its first group's precompute
+// (group_cost steps) and the launch ends about one chunk after the mean, so C
+// chunks per wave cost C * g + T / C steps for T steps per wave: C = sqrt(T /
+// g), between 4 and cap.  (32 per wave on a 1/64 shard of R=64 n=7 spent
+// about half of its time in chunk-start precomputes.)
+uint32_t chunks_per_wave(uint64_t ranks, uint32_t nwaves, uint32_t nc, uint32_t cap);
 // Expected lane utilisation of the group kernel over the whole rank space.
 double group_utilisation(uint32_t ns, uint32_t n);
 // Group-kernel geometry choice between two workgroup sizes, each with the

@@ -568,6 +568,9 @@ __global__ void __launch_bounds__(256) eval_kernel(EvalArgs a) {
 }
 
 // ----------------------------------------------------- top-K list merge --
+// (one thread per record of the G_MERGE_LISTS x KP inputs: each launch of
+// the merge chain is latency-bound, 23 us per level at 256 threads)
+constexpr int MERGE_BD = G_MERGE_LISTS * KP;
 // lists: n_lists lists, list i of objective o at src[i * list_stride + o * KP]
 // out:   one list per group of G_MERGE_LISTS lists, at dst[g * out_stride + o * KP]
 // Every input list is sorted (block top-K lists, padded with rec_max), so each
@@ -575,7 +578,7 @@ __global__ void __launch_bounds__(256) eval_kernel(EvalArgs a) {
 // plus, per other list, how many records precede it there (ties go to the
 // lower list index).  One pass of binary searches in LDS, no sort; a block
 // that finds an unsorted input falls back to the full bitonic sort.
-__global__ void __launch_bounds__(256) merge_kernel(const Rec* src, uint32_t n_lists, uint64_t list_stride, Rec* dst,
+__global__ void __launch_bounds__(1024) merge_kernel(const Rec* src, uint32_t n_lists, uint64_t list_stride, Rec* dst,
                                                      uint64_t out_stride, const Rec* alt, uint32_t alt_lists,
                                                      const unsigned long long* sel, uint64_t cap) {
   if (sel && *sel > cap) {  // device-side choice of the input (fast sweep overflow fallback)
@@ -766,7 +769,7 @@ hipError_t launch_eval(const EvalArgs& a, uint32_t n, bool full, uint32_t grid, 
 hipError_t launch_merge(const Rec* src, uint32_t n_lists, uint64_t list_stride, Rec* dst, uint64_t out_stride,
                         uint32_t n_obj, hipStream_t st) {
   uint32_t groups = (n_lists + G_MERGE_LISTS - 1) / G_MERGE_LISTS;
-  hipLaunchKernelGGL(merge_kernel, dim3(groups, n_obj), dim3(256), 0, st, src, n_lists, list_stride, dst, out_stride,
+  hipLaunchKernelGGL(merge_kernel, dim3(groups, n_obj), dim3(MERGE_BD), 0, st, src, n_lists, list_stride, dst, out_stride,
                      (const Rec*)nullptr, 0u, (const unsigned long long*)nullptr, (uint64_t)0);
   return hipGetLastError();
 }
@@ -777,7 +780,7 @@ hipError_t launch_merge_sel(const Rec* src, uint32_t n_lists, const Rec* alt, ui
   // groups cover the larger input; the surplus groups emit all-padding lists
   const uint32_t m = n_lists > alt_lists ? n_lists : alt_lists;
   uint32_t groups = (m + G_MERGE_LISTS - 1) / G_MERGE_LISTS;
-  hipLaunchKernelGGL(merge_kernel, dim3(groups, n_obj), dim3(256), 0, st, src, n_lists, list_stride, dst, out_stride,
+  hipLaunchKernelGGL(merge_kernel, dim3(groups, n_obj), dim3(MERGE_BD), 0, st, src, n_lists, list_stride, dst, out_stride,
                      alt, alt_lists, sel, cap);
   return hipGetLastError();
 }
@@ -806,31 +809,74 @@ hipError_t launch_zero_ctl(unsigned long long* counters, unsigned long long* qco
 }
 
 // The top-K seed: per objective (one block each) the K-th least of the
-// sample launch's per-chunk minima (a bitonic sort of <= 4096 keys in LDS);
-// all-ones (no bound) when fewer than K samples have the objective.
+// sample launch's per-chunk minima, by an exact MSB-first radix select (8
+// passes of 8 bits: a 256-bin LDS histogram of the keys that share the
+// prefix so far, then the digit holding the K-th); all-ones (no bound) when
+// fewer than K samples have the objective.  (A bitonic sort of the 4096 keys
+// took 56 us: 78 barrier-separated stages.)
 __global__ void __launch_bounds__(1024) seed_kernel(const uint64_t* smin, uint32_t nsamp, uint32_t K, uint64_t* tseed) {
-  __shared__ uint64_t v[4096];
+  __shared__ uint32_t hist[256];
+  __shared__ uint64_t sel[2];  // prefix, remaining rank
   const uint32_t o = blockIdx.x, tid = threadIdx.x;
-  uint32_t P = 1;
-  while (P < nsamp) P <<= 1;
-  for (uint32_t i = tid; i < P; i += blockDim.x) v[i] = i < nsamp ? smin[(size_t)o * nsamp + i] : ~0ull;
-  __syncthreads();
-  for (uint32_t k = 2; k <= P; k <<= 1) {
-    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-      for (uint32_t i = tid; i < P; i += blockDim.x) {
-        const uint32_t l = i ^ j;
-        if (l > i) {
-          const uint64_t a = v[i], b = v[l];
-          if (((i & k) == 0) == (a > b)) {
-            v[i] = b;
-            v[l] = a;
-          }
-        }
-      }
-      __syncthreads();
-    }
+  if (nsamp < K || K == 0) {
+    if (tid == 0) tseed[o] = ~0ull;
+    return;
   }
-  if (tid == 0) tseed[o] = nsamp >= K && K > 0 ? v[K - 1] : ~0ull;
+  constexpr int PER = 4;  // keys per thread (nsamp <= 4096)
+  uint64_t x[PER];
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const uint32_t k = tid + i * blockDim.x;
+    x[i] = k < nsamp ? smin[(size_t)o * nsamp + k] : ~0ull;
+  }
+  if (tid == 0) {
+    sel[0] = 0;
+    sel[1] = K;  // 1-based rank of the wanted key among those with the prefix
+  }
+  for (int pass = 7; pass >= 0; --pass) {
+    if (tid < 256) hist[tid] = 0;
+    __syncthreads();
+    const uint64_t prefix = sel[0];
+    const int sh = 8 * pass;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const uint32_t k = tid + i * blockDim.x;
+      const bool in = k < 4096 && (pass == 7 || (x[i] >> (sh + 8)) == prefix);
+      if (in) atomicAdd(&hist[(x[i] >> sh) & 0xFFu], 1u);
+    }
+    __syncthreads();
+    if (tid < 64) {  // one wave: inclusive scan of the 256 bins, 4 per lane
+      uint32_t c[4], s = 0;
+#pragma unroll
+      for (int b = 0; b < 4; ++b) c[b] = hist[4 * tid + b];
+#pragma unroll
+      for (int b = 0; b < 4; ++b) s += c[b];
+      uint32_t incl = s;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(incl, d);
+        if ((int)tid >= d) incl += y;
+      }
+      const uint64_t need = sel[1];
+      uint32_t before = incl - s;  // keys in the bins of the lanes below
+      int digit = -1;
+      uint64_t left = 0;
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        if (digit < 0 && before < need && need <= before + c[b]) {
+          digit = 4 * (int)tid + b;
+          left = need - before;
+        }
+        before += c[b];
+      }
+      if (digit >= 0) {  // exactly one lane holds the K-th key's digit
+        sel[0] = (sel[0] << 8) | (uint64_t)digit;
+        sel[1] = left;
+      }
+    }
+    __syncthreads();
+  }
+  if (tid == 0) tseed[o] = sel[0];
 }
 
 hipError_t launch_seed(const uint64_t* smin, uint32_t nsamp, uint32_t n_obj, uint32_t K, uint64_t* tseed,

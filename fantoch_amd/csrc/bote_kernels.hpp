@@ -102,6 +102,8 @@ struct FastArgs {
   uint32_t grx;       // group kernel, n <= 7: per-group position table (1) or per-lane row sorts (0)
   uint32_t keys;      // group kernel: 1 = the extended key set (n = 4..7, default objectives first)
   uint32_t gbins;     // group kernel, base key set: the member-binned client loop (bote_group.hip BN)
+  uint32_t s32;       // every sum of squares of a slot fits 32 bits (nc (2 max)^2 < 2^32): the SI group kernels keep them in 32 bits
+  uint32_t v32;       // and every V = cnt s2 - s1^2 (cnt^2 (2 max)^2 < 2^32)
   // group kernel work distribution: nwchunks > 0: waves take cost-balanced
   // rank chunks [wchunks[c], wchunks[c+1]) from ticket counters (zeroed
   // before each launch); 0: each wave sweeps an equal share of ranks.  The

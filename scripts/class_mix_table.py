@@ -1,0 +1,145 @@
+"""Per-section VALU class mix of the bench group kernel, static and modelled
+per 64-config step, reconciled against the measured SQ_INSTS_VALU.
+
+  hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -DBOTE_ISA_N7 -g \
+      --offload-device-only -S -o kg.s fantoch_amd/csrc/bote_group.hip
+  python scripts/class_mix_table.py kg.s ILi7ELb1ELb1ELb1ELb0ELb0E profiles/pmc.json r64n7_n1 > profiles/<tag>_class_mix.md
+
+Static: instructions per section (scripts/isa_lines.py markers).  Modelled
+dynamic count per step: every basic block of a per-step section runs once per
+step, except
+  * blocks on the rare paths (f64 arithmetic: COV/mean decisions inside their
+    ambiguity bands, the exact leader re-scan, the full score; the deferral
+    queue; the block top-K merge under the LDS lock; the sample launch's
+    per-chunk minima): 0;
+  * the client loop's unrolled body (the lines variant, the block with the
+    most v_dot2 and the fewest LDS reads): nq / U = 16 / 4 = 4 times, the
+    blocks laid out after it (flush, exit) once; the other client-loop bodies
+    (no-lines variant, remainder loops): 0;
+  * the block top-K merge (wave_topk, inlined; found by its own source
+    lines) and the sample launch's per-chunk minima (`if (a.smin)`): 0;
+  * per-group sections (group precompute, next group): groups / steps;
+  * per-wave and per-chunk setup: 0 (32 chunks per wave over ~2,370 steps).
+Issue cost: fast class ~1.6 wave-instr per CU-clock, slow ~0.95
+(profiles/r02_issue_rate_ops.json), so a slow op costs ~1.7 fast ones.
+"""
+import json
+import sys
+from collections import Counter, defaultdict
+
+sys.path.insert(0, __file__.rsplit("/", 1)[0])
+from isa_lines import DEFAULT_SECTIONS, parse  # noqa: E402
+from isa_mix import classify  # noqa: E402
+
+RARE_MARK = ("_f64", "v_div_", "global_atomic", "ds_cmpst", "ds_cmpswap", "s_sleep", "s_ff1", "v_rcp_f64",
+             "v_sqrt_f64")
+FAST_RATE, SLOW_RATE = 1.6, 0.95
+
+
+def main():
+    path, name = sys.argv[1], sys.argv[2]
+    pmc = json.load(open(sys.argv[3])).get(sys.argv[4]) if len(sys.argv) > 4 else None
+    groups, steps = 521855, 621216192 / 64.0  # R=64 n=7: C(ns - 1, n - 3) groups, ranks / 64
+    per_step_groups = groups / steps
+    rows = parse(path, name, raw=True)
+    secs = DEFAULT_SECTIONS
+    src = open(__file__.rsplit("/", 2)[0] + "/fantoch_amd/csrc/bote_group.hip").read().split("\n")
+    # the block top-K merge helper (inlined at its call site): rare after the seed
+    wt0 = next(i + 1 for i, l in enumerate(src) if "void wave_topk(" in l)
+    wt1 = next(i + 1 for i, l in enumerate(src) if i + 1 > wt0 and l.startswith("}"))
+    # the sample launch's per-chunk minima (a.smin): not run by the sweep launch
+    sm0 = next(i + 1 for i, l in enumerate(src) if "if (a.smin) {" in l)
+    sm1 = next(i + 1 for i, l in enumerate(src) if i + 1 > sm0 and "} else if (!ABLATE(a, 4)) {" in l)
+    blk_ops = defaultdict(list)
+    blk_lines = defaultdict(Counter)
+    merge_blk = set()
+    own_line = defaultdict(bool)  # a block with instructions from bote_group.hip lines
+    order = []
+    for ln, b, op, raw_ln in rows:
+        if b not in blk_ops:
+            order.append(b)
+        blk_ops[b].append(op)
+        own_line[b] |= raw_ln > 0
+        if wt0 <= raw_ln <= wt1 or sm0 <= raw_ln < sm1:
+            merge_blk.add(b)
+        if ln:
+            s = next((n for n, a, z in secs if a <= ln <= z), "other")
+            blk_lines[b][s] += 1
+    sec_of = {b: (blk_lines[b].most_common(1)[0][0] if blk_lines[b] else "other") for b in order}
+    # the client loop's hot body (the lines variant: the block with the most
+    # v_dot2 and the fewest LDS reads), and the run of client-loop blocks laid
+    # out with it (its flush and exit); the other variants (no lines, the
+    # remainder loops) do not run at R=64 n=7 (<= 16 pairs per step, nq % 4 == 0)
+    loop_blocks = [b for b in order if sec_of[b].startswith("client loop")]
+    dots = {b: sum(1 for o in blk_ops[b] if o.startswith("v_dot2")) for b in loop_blocks}
+    big = [b for b in loop_blocks if dots[b] >= 16]
+    hot = min(big, key=lambda b: sum(1 for o in blk_ops[b] if o.startswith("ds_"))) if big else None
+    run = set()
+    if hot:
+        i = order.index(hot)
+        while i < len(order) and sec_of[order[i]].startswith("client loop"):
+            run.add(order[i])
+            i += 1
+    static = defaultdict(Counter)
+    dyn = defaultdict(Counter)
+    for b in order:
+        s = sec_of[b]
+        c = Counter(classify(o) for o in blk_ops[b])
+        static[s].update(c)
+        # (top-K blocks made only of header code: the merge's inlined binary searches)
+        rare = (b in merge_blk or any(m in o for o in blk_ops[b] for m in RARE_MARK) or
+                (s.startswith("top-K") and not own_line[b]))
+        if s.startswith("setup") or s == "other" or rare:
+            w = 0.0
+        elif s in ("group precompute", "next group"):
+            w = per_step_groups
+        elif s.startswith("client loop"):
+            w = 4.0 if b == hot else (1.0 if b in run else 0.0)
+        else:
+            w = 1.0
+        for k, v in c.items():
+            dyn[s][k] += w * v
+    print(f"# VALU class mix per section: `{name}`\n")
+    print("Static instructions from the device assembly (`-g` line info, scripts/isa_lines.py sections);")
+    print("modelled per 64-config step as described in scripts/class_mix_table.py.  Fast class")
+    print(f"~{FAST_RATE} wave-instr/CU-clk, slow ~{SLOW_RATE} (profiles/r02_issue_rate_ops.json).\n")
+    print("| section | static fast | static slow | per step fast | per step slow | per step spill-lane | "
+          "issue cost (fast-op units) | share |")
+    print("|---|---|---|---|---|---|---|---|")
+    tot = Counter()
+    costs = {}
+    for s, _, _ in secs + [("other", 0, 0)]:
+        d = dyn.get(s, Counter())
+        costs[s] = d["valu_fast"] + d["valu_slow"] * FAST_RATE / SLOW_RATE + d["spill_lane"] * FAST_RATE / SLOW_RATE
+    allc = sum(costs.values()) or 1.0
+    for s, _, _ in secs + [("other", 0, 0)]:
+        st, d = static.get(s, Counter()), dyn.get(s, Counter())
+        if not st:
+            continue
+        tot.update(d)
+        print(f"| {s} | {st['valu_fast']} | {st['valu_slow']} | {d['valu_fast']:.1f} | {d['valu_slow']:.1f} | "
+              f"{d['spill_lane']:.1f} | {costs[s]:.0f} | {costs[s] / allc:.1%} |")
+    model = tot["valu_fast"] + tot["valu_slow"] + tot["spill_lane"]
+    print(f"| **total** | | | {tot['valu_fast']:.0f} | {tot['valu_slow']:.0f} | {tot['spill_lane']:.0f} | "
+          f"{allc:.0f} | |\n")
+    print(f"Modelled VALU instructions per step (fast + slow + spill-lane moves): **{model:.0f}**; "
+          f"slow share {(tot['valu_slow'] + tot['spill_lane']) / model:.1%}.")
+    if pmc:
+        meas = pmc["valu_insts_per_config"]
+        # wavefront steps actually run per 64 configs: a group of C(p3, 3) configs takes ceil(/64) steps
+        from math import comb, ceil
+        ns, n = 64, 7
+        real = sum(comb(ns - 1 - p3, n - 4) * ceil(comb(p3, 3) / 64) for p3 in range(3, ns)) / (comb(ns, n) / 64)
+        print(f"Measured SQ_INSTS_VALU per 64 configs ({pmc['source']}): **{meas:.0f}**.  Groups run "
+              f"{real:.3f} steps per 64 configs (partial last steps), so the model accounts for "
+              f"{model * real:.0f} = {model * real / meas:.0%} of it; the rest is the rare paths (f64 "
+              f"decisions inside their bands, leader re-scans, block top-K merges), which run for a whole "
+              f"wavefront when any lane takes them, and per-chunk work.")
+        ceil = 1.0 / (tot["valu_fast"] / model / FAST_RATE + (1 - tot["valu_fast"] / model) / SLOW_RATE) / 2.0
+        print(f"Issue ceiling of this mix: {ceil:.1%} of the 2-cycle nominal rate; measured "
+              f"{pmc['valu_issue_util']:.1%} ({pmc['valu_issue_util'] / ceil:.0%} of the ceiling).")
+    print(f"\nClient-loop hot body: `{hot}` ({len(blk_ops[hot]) if hot else 0} instructions for 4 quads = 16 clients).")
+
+
+if __name__ == "__main__":
+    main()

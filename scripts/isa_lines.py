@@ -21,10 +21,9 @@ from isa_mix import classify  # noqa: E402
 
 # lines of bote_group.hip before the kernel body are helpers (inlined):
 # charged, like header code, to the call site
-BODY_FIRST = 350
 
 
-def parse(path, name):
+def parse(path, name, raw=False):
     lines = open(path).read().split("\n")
     files = {}
     start = None
@@ -55,27 +54,43 @@ def parse(path, name):
             continue
         if not s or s.startswith(";") or s.startswith("."):
             continue
-        out.append((main_line, block, s.split()[0]))
+        out.append((main_line, block, s.split()[0]) if not raw else
+                   (main_line, block, s.split()[0], cur_line if files.get(cur_file, "").endswith("bote_group.hip") else 0))
     return out
 
 
-DEFAULT_SECTIONS = [
-    ("setup+chunks", 350, 491),
-    ("group precompute", 492, 562),
-    ("step head (lowtab, keys init)", 563, 587),
-    ("client lines build", 588, 627),
-    ("Q phase (rows, merges)", 628, 847),
-    ("byte planes + colocated sums", 848, 869),
-    ("leader choice", 870, 942),
-    ("XK all leaders", 943, 992),
-    ("client loop (Input leaderless)", 993, 1143),
-    ("FPaxos + colocated moments", 1144, 1188),
-    ("validity", 1189, 1237),
-    ("digest", 1238, 1248),
-    ("objective keys + score", 1249, 1315),
-    ("top-K screen + merge", 1316, 1327),
-    ("next group", 1328, 1400),
+# Sections start at marker text in bote_group.hip (so they follow edits)
+MARKERS = [
+    ("setup+chunks", "sweep_group_kernel(FastArgs a) {"),
+    ("group precompute", "// ---------------- per-group, wave-uniform precompute"),
+    ("step head (lowtab, keys init)", "// ---------------- the group's configs, 64 per step"),
+    ("client lines build", "// ---- PERM: client lines."),
+    ("Q phase (rows, merges)", "uint32_t pv[3], rv[3];"),
+    ("byte planes + colocated sums", "// ---- PERM: byte planes"),
+    ("leader choice", "// ---- FPaxos leader (f = 1"),
+    ("XK all leaders", "// ---- XK, before the client loop"),
+    ("client loop (Input leaderless)", "// ---- Input leaderless: 3 lane columns"),
+    ("FPaxos + colocated moments", "// ---- Input FPaxos from the leader column's sums"),
+    ("validity", "// af1's exact V"),
+    ("digest", "if ((SI || a.want_digest) && !ABLATE(a, 16))"),
+    ("objective keys + score", "// ---- default objectives: 0 SCORE"),
+    ("top-K screen + merge", "// ---- top-K: lock-free screen"),
+    ("next group", "// ---------------- next group"),
+    (None, "// ------------------------------------------------------------- launcher"),
 ]
+
+
+def default_sections():
+    src = open(__file__.rsplit("/", 2)[0] + "/fantoch_amd/csrc/bote_group.hip").read().split("\n")
+    starts = []
+    for name, text in MARKERS:
+        ln = next(i + 1 for i, l in enumerate(src) if text in l)
+        starts.append((name, ln))
+    return [(n, a, starts[k + 1][1] - 1) for k, (n, a) in enumerate(starts[:-1])]
+
+
+DEFAULT_SECTIONS = default_sections()
+BODY_FIRST = DEFAULT_SECTIONS[0][1]
 
 
 def main():

@@ -23,7 +23,7 @@ for mask in [int(x, 0) for x in sys.argv[1:]] or [0, 4]:
     os.environ["BOTE_ABLATE"] = str(mask)
     sw = Sweep(dp, srv, srv, 7, DEFAULT_OBJECTIVES, K=100, ranking=DEFAULT_RANKING, digest=True)
     row = []
-    for parts in (1, 8, 64):
+    for parts in (1, 2, 4, 8, 64):
         b = sw.split(0, sw.total, parts)
         i = parts // 2
         sw.launch(b[i], b[i + 1])

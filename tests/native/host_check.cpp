@@ -227,7 +227,20 @@ static void check_geometry() {
   CHECK(!pick_group_geometry(256, 0, 0, 0, 0, 0));
 }
 
+// Chunks per wave (sweep_chunks): the cap on full sweeps, fewer on shards.
+static void check_chunks_per_wave() {
+  // R=64 n=7 on 4096 waves, 64 clients (group cost 0.64 steps)
+  CHECK(chunks_per_wave(621216192ull, 4096, 64, 32) == 32);
+  CHECK(chunks_per_wave(621216192ull / 8, 4096, 64, 32) == 22);
+  CHECK(chunks_per_wave(621216192ull / 64, 4096, 64, 32) == 8);
+  CHECK(chunks_per_wave(1000, 4096, 64, 32) == 4);
+  CHECK(chunks_per_wave(5423611200ull, 4096, 128, 32) == 32);
+  CHECK(chunks_per_wave(1ull << 40, 0, 64, 32) == 4);
+  CHECK(chunks_per_wave(1ull << 40, 4096, 64, 2) == 2);
+}
+
 int main() {
+  check_chunks_per_wave();
   check_geometry();
   check_binomials();
   check_unrank();
