@@ -1118,10 +1118,15 @@ static int launch_generic(bote_sweep* s, uint64_t rb, uint64_t re, hipStream_t s
 
 // The top-K seed of a group launch over [rb, re) (launch_fast_path): sets
 // f.tseed, or leaves it null when the range is too small to sample.
+#ifndef BOTE_SEED_STEPS
+#define BOTE_SEED_STEPS 8  // sample steps per wave (r03v A/B: 8 vs 1, kernel -1.6 %, 1/8 shard -5 %)
+#endif
 static int sample_seed(bote_sweep* s, bote::FastArgs& f, uint64_t rb, uint64_t re, hipStream_t st) {
   const uint32_t nwaves = s->fgrid * (s->fargs.gbd / 64);
-  const uint32_t nsamp = std::min<uint32_t>(4096, nwaves);
+  const uint32_t base = std::min<uint32_t>(4096, nwaves);
   // samples are disjoint one-step chunks and at most 1/8 of the range
+  const uint64_t fit = (re - rb) / (64 * 8);
+  const uint32_t nsamp = (uint32_t)std::min<uint64_t>({(uint64_t)base * BOTE_SEED_STEPS, std::max<uint64_t>(base, fit), 65536});
   if (nsamp < s->K || re - rb < (uint64_t)nsamp * 64 * 8) return BOTE_OK;
   auto key = std::make_pair(rb, re);
   auto it = s->samples.find(key);

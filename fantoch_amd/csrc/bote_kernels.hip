@@ -809,40 +809,63 @@ hipError_t launch_zero_ctl(unsigned long long* counters, unsigned long long* qco
 }
 
 // The top-K seed: per objective (one block each) the K-th least of the
-// sample launch's per-chunk minima, by an exact MSB-first radix select (8
-// passes of 8 bits: a 256-bin LDS histogram of the keys that share the
-// prefix so far, then the digit holding the K-th); all-ones (no bound) when
-// fewer than K samples have the objective.  (A bitonic sort of the 4096 keys
-// took 56 us: 78 barrier-separated stages.)
+// sample launch's per-chunk minima, by an exact MSB-first radix select (8-bit
+// digits: a 256-bin LDS histogram of the keys that share the prefix so far,
+// then the digit holding the K-th); all-ones (no bound) when fewer than K
+// samples have the objective.  The bytes above the highest one in which the
+// keys differ (found first from their AND and OR) are taken as known: mean
+// keys (S1 < 2^21) skip 5 of the 8 passes, whose histograms would all hit one
+// bin.  (A bitonic sort of 4096 keys took 56 us: 78 barrier-separated stages.)
 __global__ void __launch_bounds__(1024) seed_kernel(const uint64_t* smin, uint32_t nsamp, uint32_t K, uint64_t* tseed) {
   __shared__ uint32_t hist[256];
   __shared__ uint64_t sel[2];  // prefix, remaining rank
-  const uint32_t o = blockIdx.x, tid = threadIdx.x;
+  __shared__ uint64_t red[2][16];
+  const uint32_t o = blockIdx.x, tid = threadIdx.x, BD = blockDim.x;
   if (nsamp < K || K == 0) {
     if (tid == 0) tseed[o] = ~0ull;
     return;
   }
-  constexpr int PER = 4;  // keys per thread (nsamp <= 4096)
-  uint64_t x[PER];
+  const uint64_t* x = smin + (size_t)o * nsamp;
+  // the AND and OR of all keys: the bits above their highest difference are common
+  uint64_t va = ~0ull, vo = 0;
+  for (uint32_t k = tid; k < nsamp; k += BD) {
+    va &= x[k];
+    vo |= x[k];
+  }
 #pragma unroll
-  for (int i = 0; i < PER; ++i) {
-    const uint32_t k = tid + i * blockDim.x;
-    x[i] = k < nsamp ? smin[(size_t)o * nsamp + k] : ~0ull;
+  for (int d = 32; d >= 1; d >>= 1) {
+    va &= (uint64_t)__shfl_xor((long long)va, d);
+    vo |= (uint64_t)__shfl_xor((long long)vo, d);
   }
+  if ((tid & 63) == 0) {
+    red[0][tid >> 6] = va;
+    red[1][tid >> 6] = vo;
+  }
+  __syncthreads();
   if (tid == 0) {
-    sel[0] = 0;
-    sel[1] = K;  // 1-based rank of the wanted key among those with the prefix
+    uint64_t a = ~0ull, b = 0;
+    for (uint32_t w = 0; w < (BD >> 6); ++w) {
+      a &= red[0][w];
+      b |= red[1][w];
+    }
+    const uint64_t diff = a ^ b;  // bits in which some keys differ
+    const int top = diff ? 63 - __clzll(diff) : -1;  // highest such bit
+    const int pass0 = top < 0 ? -1 : top / 8;        // first byte to select on
+    // the known high bytes; the rank within them is K
+    sel[0] = pass0 < 0 ? a : (pass0 == 7 ? 0 : a >> (8 * (pass0 + 1)));
+    sel[1] = K;
+    red[0][0] = (uint64_t)(int64_t)pass0;
   }
-  for (int pass = 7; pass >= 0; --pass) {
+  __syncthreads();
+  const int pass0 = (int)(int64_t)red[0][0];
+  for (int pass = pass0; pass >= 0; --pass) {
     if (tid < 256) hist[tid] = 0;
     __syncthreads();
     const uint64_t prefix = sel[0];
     const int sh = 8 * pass;
-#pragma unroll
-    for (int i = 0; i < PER; ++i) {
-      const uint32_t k = tid + i * blockDim.x;
-      const bool in = k < 4096 && (pass == 7 || (x[i] >> (sh + 8)) == prefix);
-      if (in) atomicAdd(&hist[(x[i] >> sh) & 0xFFu], 1u);
+    for (uint32_t k = tid; k < nsamp; k += BD) {
+      const uint64_t v = x[k];
+      if (pass == 7 || (v >> (sh + 8)) == prefix) atomicAdd(&hist[(v >> sh) & 0xFFu], 1u);
     }
     __syncthreads();
     if (tid < 64) {  // one wave: inclusive scan of the 256 bins, 4 per lane
@@ -881,7 +904,6 @@ __global__ void __launch_bounds__(1024) seed_kernel(const uint64_t* smin, uint32
 
 hipError_t launch_seed(const uint64_t* smin, uint32_t nsamp, uint32_t n_obj, uint32_t K, uint64_t* tseed,
                        hipStream_t st) {
-  if (nsamp > 4096) return hipErrorInvalidValue;
   hipLaunchKernelGGL(seed_kernel, dim3(n_obj), dim3(1024), 0, st, smin, nsamp, K, tseed);
   return hipGetLastError();
 }
