@@ -496,7 +496,7 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
     if (lane == 0) cnext = atomicAdd(tctr, 1u);
     chunk = c;
     r = uni64(a.wchunks[c]);
-    rend = a.smin ? min(r + 64, a.re) : uni64(a.wchunks[c + 1]);  // (sample chunks: one step each)
+    rend = a.smin ? min(r + 64ull * a.ssteps, a.re) : uni64(a.wchunks[c + 1]);  // (sample chunks: ssteps steps)
     GASSERT(a, a.rb <= r && r <= rend && rend <= a.re, 0);  // chunk inside the launch range
   } else {
     if (static_done) break;

@@ -118,13 +118,14 @@ struct FastArgs {
   // then those positions as bytes (16 at most); null: unranked on the device
   const uint64_t* wstate;
   // top-K seed (bote_capi.hip launch_fast_path): the sample launch (smin
-  // non-null) takes nwchunks one-step chunks at wchunks[c] and records, per
+  // non-null) takes nwchunks chunks of ssteps steps at wchunks[c] and records, per
   // objective o, the least key of chunk c at smin[o * nwchunks + c] (no lists,
   // counters or deferrals); seed_kernel turns those into tseed[o], the K-th
   // least, a bound on the launch's K-th key that the main launch starts its
   // thresholds at
   uint64_t* smin;
   const uint64_t* tseed;
+  uint32_t ssteps;  // sample launch: steps (of 64 configs) per sample chunk
   int want_score, p_int;
   int64_t p1i, p2i;  // p_int: min_mean_{fpaxos,epaxos}_improv * nc as integers
   // group kernel mean tests on D = the integer difference of two sums: true
