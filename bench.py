@@ -281,7 +281,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
     # a timing-diagnostics environment must not produce a bench line
-    for var in ("BOTE_ABLATE", "BOTE_SWEEP_KERNEL", "BOTE_FORCE_GENERIC", "BOTE_NO_DEF_OBJ"):
+    for var in ("BOTE_ABLATE", "BOTE_SWEEP_KERNEL", "BOTE_FORCE_GENERIC", "BOTE_NO_DEF_OBJ", "BOTE_CHUNKS_PER_WAVE"):
         if os.environ.get(var):
             sys.exit(f"bench.py: refusing to run with {var} set (diagnostics only)")
 
