@@ -289,15 +289,14 @@ def main():
     if args.gpus < 1:
         sys.exit("bench.py: --gpus must be >= 1")
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
-        # launcher: start the N ranks and exit with their status.  Counting
-        # devices does not initialise HIP (no GPU call in this process).
-        import torch
+        # launcher: start the N ranks and exit with their status.  This
+        # process never initialises HIP: the GPUs are counted in a child.
+        from fantoch_amd.launch import count_gpus, run_world
 
-        ndev = torch.cuda.device_count()
+        ndev = count_gpus()
         if ndev < args.gpus and not (rehearsal and ndev >= 1):
             sys.exit(f"bench.py: --gpus {args.gpus} but {ndev} GPU(s) visible; refusing to report "
                      f"{args.gpus} GPUs")
-        from fantoch_amd.launch import run_world
 
         sys.exit(run_world(args.gpus, [os.path.abspath(__file__)] + sys.argv[1:]))
 
@@ -319,10 +318,18 @@ def main():
     dev_index = local % max(ndev, 1) if rehearsal else local
     torch.cuda.set_device(dev_index)
     if world > 1:
-        if rehearsal:
-            dist.init_process_group("gloo")
-        else:
-            dist.init_process_group("nccl", device_id=torch.device("cuda", dev_index))
+        try:
+            if rehearsal:
+                dist.init_process_group("gloo")
+            else:
+                dist.init_process_group("nccl", device_id=torch.device("cuda", dev_index))
+        except Exception as ex:  # (rank 0's store could not bind MASTER_PORT: the launcher retries)
+            if "address already in use" in str(ex).lower() or "eaddrinuse" in str(ex).lower():
+                from fantoch_amd.launch import PORT_IN_USE
+
+                print(f"bench.py rank {rank}: {ex}", file=sys.stderr)
+                sys.exit(PORT_IN_USE)
+            raise
 
     from fantoch_amd import _lib
     from fantoch_amd.bote import CONFIG5_OBJECTIVES, DEFAULT_OBJECTIVES, DEFAULT_RANKING, DevicePlanet, Sweep

@@ -176,6 +176,21 @@ constexpr uint64_t QUEUE_CAP = 1ull << 20;  // deferred near-tie configs per lau
 #endif
 }  // namespace
 
+// Restores the calling thread's current HIP device when an entry returns:
+// the entries switch to their planet's device, and the library must not
+// leave the caller (a Rust or PyTorch host on another device) switched.
+struct DevGuard {
+  int dev = -1;
+  DevGuard() {
+    if (hipGetDevice(&dev) != hipSuccess) dev = -1;
+  }
+  ~DevGuard() {
+    if (dev >= 0) (void)hipSetDevice(dev);
+  }
+  DevGuard(const DevGuard&) = delete;
+  DevGuard& operator=(const DevGuard&) = delete;
+};
+
 extern "C" {
 
 const char* bote_last_error(void) { return g_err.c_str(); }
@@ -191,6 +206,7 @@ int bote_device_count(int* out) {
 
 // ------------------------------------------------------------------ planet
 int bote_planet_create(const uint16_t* lat, uint32_t R, int device, bote_planet** out) {
+  DevGuard dev_guard;  // the caller's current device is restored on return
   if (!lat || !out) return fail(BOTE_E_ARG, "null argument");
   if (R == 0 || R > BOTE_MAX_REGIONS) return fail(BOTE_E_RANGE, "R must be in [1, 128]");
   for (size_t i = 0; i < (size_t)R * R; ++i)
@@ -220,6 +236,7 @@ int bote_planet_create(const uint16_t* lat, uint32_t R, int device, bote_planet*
 }
 
 int bote_planet_destroy(bote_planet* p) {
+  DevGuard dev_guard;  // the caller's current device is restored on return
   if (!p) return BOTE_OK;
   (void)hipSetDevice(p->device);
   if (p->stream) (void)hipStreamSynchronize(p->stream);
@@ -261,6 +278,7 @@ int bote_colex_unrank(uint64_t rank, uint32_t n, uint32_t ns, uint32_t* out) {
 static int run_single(const bote_planet* p, const uint32_t* servers, uint32_t ns, const uint32_t* clients, uint32_t nc,
                       const uint32_t* froms, uint32_t nf, uint32_t q, uint32_t leader, int mode, uint64_t* out,
                       size_t nout) {
+  DevGuard dev_guard;  // the caller's current device is restored on return
   if (!p || !out) return fail(BOTE_E_ARG, "null argument");
   int rc;
   if ((rc = check_regions(servers, ns, p->R, false, "servers"))) return rc;
@@ -320,6 +338,7 @@ int bote_all_leaders(const bote_planet* p, const uint32_t* servers, uint32_t ns,
 
 int bote_best_leader(const bote_planet* p, const uint32_t* servers, uint32_t ns, const uint32_t* clients, uint32_t nc,
                      uint32_t q, int stat, uint32_t* out_pos, uint64_t* out_lat) {
+  DevGuard dev_guard;  // the caller's current device is restored on return
   if (!p || !out_pos) return fail(BOTE_E_ARG, "null argument");
   if (ns == 0) return fail(BOTE_E_ARG, "the best leader should exist (empty server list)");
   if (stat < 0 || stat > 2) return fail(BOTE_E_ARG, "unknown stat");
@@ -391,6 +410,7 @@ static int eval_impl(const bote_planet* p, const uint32_t* servers, uint32_t ns,
                      const bote_ranking_params* rp, uint32_t keys, uint32_t* out_vals, uint32_t* out_leader,
                      uint64_t* out_sum, uint64_t* out_sumsq, double* out_mean, double* out_cov, double* out_score,
                      uint8_t* out_valid, uint64_t* out_al_sum, uint64_t* out_al_sumsq) {
+  DevGuard dev_guard;  // the caller's current device is restored on return
   int rc;
   if (keys > BOTE_KEYS_TEMPO_ALL_LEADERS) return fail(BOTE_E_ARG, "unknown key set");
   if ((rc = check_search_args(p, servers, ns, clients, nc, n))) return rc;
@@ -506,6 +526,7 @@ int bote_eval_leaderless(const bote_planet* p, const uint32_t* servers, uint32_t
                          uint32_t nc, uint32_t n, const uint32_t* configs, uint64_t rank_begin, uint64_t ncfg,
                          const uint32_t* quorum_sizes, uint32_t nq, uint32_t* out_vals, uint64_t* out_sum,
                          uint64_t* out_sumsq) {
+  DevGuard dev_guard;  // the caller's current device is restored on return
   int rc;
   if (!p) return fail(BOTE_E_ARG, "planet is null");
   if (n < 1 || n > BOTE_MAX_N) return fail(BOTE_E_RANGE, "config size must be in [1, 16]");
@@ -585,6 +606,7 @@ int bote_eval_leaderless(const bote_planet* p, const uint32_t* servers, uint32_t
 int bote_evolving_chains(int device, uint32_t ns, const uint32_t* counts, const uint64_t* const* masks,
                          const double* const* scores, const double* const* means, double min_mean_decrease,
                          int ft_metric, uint64_t max_out, uint32_t* out_idx, double* out_score, uint64_t* out_total) {
+  DevGuard dev_guard;  // the caller's current device is restored on return
   if (!counts || !masks || !scores || !means || !out_total) return fail(BOTE_E_ARG, "null argument");
   if (ns == 0 || ns > 64) return fail(BOTE_E_RANGE, "the server list must hold 1 to 64 regions");
   if (ft_metric != BOTE_FT_F1 && ft_metric != BOTE_FT_F1F2) return fail(BOTE_E_ARG, "bad ft_metric");
@@ -644,6 +666,7 @@ static bool slot_exists_n(uint32_t n, uint32_t slot, uint32_t keys) {
 int bote_sweep_create_keys(const bote_planet* p, const uint32_t* servers, uint32_t ns, const uint32_t* clients,
                            uint32_t nc, uint32_t n, const bote_objective* objs, uint32_t n_obj, uint32_t K,
                            const bote_ranking_params* rp, int digest, int kernel, uint32_t keys, bote_sweep** out) {
+  DevGuard dev_guard;  // the caller's current device is restored on return
   int rc;
   if (!out) return fail(BOTE_E_ARG, "out is null");
   if (keys > BOTE_KEYS_TEMPO_ALL_LEADERS) return fail(BOTE_E_ARG, "unknown key set");
@@ -744,7 +767,7 @@ int bote_sweep_create_keys(const bote_planet* p, const uint32_t* servers, uint32
                       (uint64_t)nc * (16 * maxlat_all + 15) < (1ull << 24) &&
                       2 * (16 * maxlat_all + 15) * (16 * maxlat_all + 15) < (1ull << 32);
   if (keys && s->fast &&
-      (!bote::group_supports_keys(n, 256) || !keys_def || !keys32 || kernel == BOTE_KERNEL_FAST)) {
+      (!bote::group_supports_keys(n, bote::GROUP_XK_MAX_BD) || !keys_def || !keys32 || kernel == BOTE_KERNEL_FAST)) {
     if (kernel == BOTE_KERNEL_FAST || kernel == BOTE_KERNEL_GROUP)
       return cleanup(fail(BOTE_E_ARG, "the extended key set runs on the group kernel (n = 4..7, config 5's "
                                       "objectives) or the generic kernel"));
@@ -1256,6 +1279,7 @@ static int launch_fast_path(bote_sweep* s, uint64_t rb, uint64_t re, hipStream_t
 }
 
 int bote_sweep_launch(bote_sweep* s, uint64_t rank_begin, uint64_t rank_end, void* hip_stream) {
+  DevGuard dev_guard;  // the caller's current device is restored on return
   if (!s) return fail(BOTE_E_ARG, "sweep is null");
   uint64_t total = binom_u64(s->ns, s->n);
   if (rank_begin > rank_end || rank_end > total) return fail(BOTE_E_ARG, "rank range out of bounds");
@@ -1273,6 +1297,7 @@ int bote_sweep_launch(bote_sweep* s, uint64_t rank_begin, uint64_t rank_end, voi
 uint64_t bote_sweep_result_bytes(const bote_sweep* s) { return s ? s->result_bytes() : 0; }
 
 int bote_sweep_result_device(bote_sweep* s, void* dst, void* hip_stream) {
+  DevGuard dev_guard;  // the caller's current device is restored on return
   if (!s || !dst) return fail(BOTE_E_ARG, "null argument");
   if (!s->launched) return fail(BOTE_E_ARG, "sweep not launched");
   HIP_TRY(hipSetDevice(s->p->device));
@@ -1289,6 +1314,7 @@ static void unpack_result(const bote_sweep* s, const std::vector<uint8_t>& blk, 
 
 int bote_sweep_result(bote_sweep* s, void* hip_stream, bote_topk_record* out, uint32_t* out_count,
                       uint64_t* out_valid, uint64_t* out_digest) {
+  DevGuard dev_guard;  // the caller's current device is restored on return
   if (!s) return fail(BOTE_E_ARG, "sweep is null");
   if (!s->launched) return fail(BOTE_E_ARG, "sweep not launched");
   HIP_TRY(hipSetDevice(s->p->device));
@@ -1307,6 +1333,7 @@ int bote_sweep_result(bote_sweep* s, void* hip_stream, bote_topk_record* out, ui
 }
 
 int bote_merge_device(const bote_sweep* s, const void* src, uint32_t n_shards, void* dst, void* hip_stream) {
+  DevGuard dev_guard;  // the caller's current device is restored on return
   if (!s || !src || !dst || n_shards == 0) return fail(BOTE_E_ARG, "bad merge arguments");
   if (n_shards > bote::G_MERGE_LISTS) return fail(BOTE_E_RANGE, "at most 8 shards per merge call");
   HIP_TRY(hipSetDevice(s->p->device));
@@ -1334,6 +1361,7 @@ int bote_sweep_timing_reset(bote_sweep* s) {
 }
 
 int bote_sweep_timing(bote_sweep* s, float* out_total_ms, uint32_t* out_launches) {
+  DevGuard dev_guard;  // the caller's current device is restored on return
   if (!s || !out_total_ms || !out_launches) return fail(BOTE_E_ARG, "null argument");
   HIP_TRY(hipSetDevice(s->p->device));
   float tot = 0.f;
@@ -1349,6 +1377,7 @@ int bote_sweep_timing(bote_sweep* s, float* out_total_ms, uint32_t* out_launches
 }
 
 int bote_sweep_deferred(bote_sweep* s, void* hip_stream, uint64_t* out) {
+  DevGuard dev_guard;  // the caller's current device is restored on return
   if (!s || !out) return fail(BOTE_E_ARG, "null argument");
   *out = 0;
   if (!s->fast || !s->launched) return BOTE_OK;
@@ -1369,6 +1398,7 @@ int bote_sweep_grid(const bote_sweep* s, uint32_t* out_grid, uint32_t* out_block
 }
 
 int bote_sweep_destroy(bote_sweep* s) {
+  DevGuard dev_guard;  // the caller's current device is restored on return
   if (!s) return BOTE_OK;
   (void)hipSetDevice(s->p ? s->p->device : 0);
   for (auto& e : s->evpool) {
@@ -1406,6 +1436,10 @@ struct bote_search {
   std::vector<Shard> sh;
   int root = 0;
   hipStream_t rst = nullptr;
+  // recorded on rst after a launch's last merge: the next launch's shard
+  // streams wait on it before they overwrite `gathered` (a launch may follow
+  // a launch without a result() between them)
+  hipEvent_t merged_ev = nullptr;
   DBuf gathered, bufa, bufb, merged;
   uint64_t nb = 0;
   uint64_t rb = 0, re = 0;
@@ -1415,6 +1449,7 @@ struct bote_search {
 namespace {
 // Drains every stream of the handle, then frees it (any state, error paths too).
 void search_free(bote_search* h) {
+  DevGuard dev_guard;  // the caller's current device is restored on return
   if (!h) return;
   for (auto& x : h->sh) {
     if (x.st) {
@@ -1426,6 +1461,10 @@ void search_free(bote_search* h) {
     (void)hipSetDevice(h->root);
     (void)hipStreamSynchronize(h->rst);
     (void)hipStreamDestroy(h->rst);
+  }
+  if (h->merged_ev) {
+    (void)hipSetDevice(h->root);
+    (void)hipEventDestroy(h->merged_ev);
   }
   for (auto& x : h->sh) {
     (void)hipSetDevice(x.dev);
@@ -1448,6 +1487,7 @@ int bote_search_create(const bote_planet* const* planets, uint32_t n_devices, co
                        const uint32_t* clients, uint32_t nc, uint32_t n, uint64_t rank_begin, uint64_t rank_end,
                        const bote_objective* objs, uint32_t n_obj, uint32_t K, const bote_ranking_params* rp,
                        int digest, uint32_t keys, bote_search** out) {
+  DevGuard dev_guard;  // the caller's current device is restored on return
   if (!out) return fail(BOTE_E_ARG, "out is null");
   *out = nullptr;
   if (!planets || n_devices == 0) return fail(BOTE_E_ARG, "no planets");
@@ -1500,8 +1540,9 @@ int bote_search_create(const bote_planet* const* planets, uint32_t n_devices, co
   h->nb = h->sh[0].sw->result_bytes();
   const size_t groups = (n_devices + bote::G_MERGE_LISTS - 1) / bote::G_MERGE_LISTS;
   if ((e = hipSetDevice(h->root)) != hipSuccess) return cleanup(hip_fail(e, "hipSetDevice (root)"));
-  if ((e = hipStreamCreateWithFlags(&h->rst, hipStreamNonBlocking)) != hipSuccess)
-    return cleanup(hip_fail(e, "root stream"));
+  if ((e = hipStreamCreateWithFlags(&h->rst, hipStreamNonBlocking)) != hipSuccess ||
+      (e = hipEventCreateWithFlags(&h->merged_ev, hipEventDisableTiming)) != hipSuccess)
+    return cleanup(hip_fail(e, "root stream/event"));
   if (h->gathered.alloc(h->nb * n_devices) != hipSuccess || h->bufa.alloc(h->nb * groups) != hipSuccess ||
       h->bufb.alloc(h->nb * groups) != hipSuccess || h->merged.alloc(h->nb) != hipSuccess)
     return cleanup(fail(BOTE_E_NOMEM, "gather buffers"));
@@ -1529,6 +1570,7 @@ int bote_search_bounds(const bote_search* h, uint64_t* out_bounds) {
 }
 
 int bote_search_launch(bote_search* h) {
+  DevGuard dev_guard;  // the caller's current device is restored on return
   if (!h) return fail(BOTE_E_ARG, "search is null");
   int rc;
   hipError_t e;
@@ -1539,6 +1581,11 @@ int bote_search_launch(bote_search* h) {
   for (uint32_t i = 0; i < nd; ++i) {
     auto& x = h->sh[i];
     char* dst = h->gathered.as<char>() + h->nb * i;
+    // (write-after-read: the previous launch's merge tree may still be reading `gathered`)
+    if (h->launched) {
+      if ((e = hipSetDevice(x.dev)) != hipSuccess || (e = hipStreamWaitEvent(x.st, h->merged_ev, 0)) != hipSuccess)
+        return hip_fail(e, "wait for the previous merge");
+    }
     if (x.dev == h->root) {
       if ((rc = bote_sweep_result_device(x.sw, dst, x.st))) return rc;
     } else {
@@ -1571,12 +1618,14 @@ int bote_search_launch(bote_search* h) {
     m = groups;
   }
   if ((rc = bote_merge_device(s0, src, m, h->merged.p, h->rst))) return rc;
+  if ((e = hipEventRecord(h->merged_ev, h->rst)) != hipSuccess) return hip_fail(e, "record merge event");
   h->launched = true;
   return BOTE_OK;
 }
 
 int bote_search_result(bote_search* h, bote_topk_record* out, uint32_t* out_count, uint64_t* out_valid,
                        uint64_t* out_digest) {
+  DevGuard dev_guard;  // the caller's current device is restored on return
   if (!h) return fail(BOTE_E_ARG, "search is null");
   if (!h->launched) return fail(BOTE_E_ARG, "search not launched");
   HIP_TRY(hipSetDevice(h->root));

@@ -283,24 +283,46 @@ __device__ __forceinline__ uint64_t cov_key(const Mom& m) {
   return (uint64_t)__double_as_longlong(rr);
 }
 
-// Per-config digest (DESIGN.md "Digest"), summed over configs mod 2^64:
-//   h = 0; for each present slot s ascending:
-//     h = (h ^ lo32(s1_s)) * 0x9E3779B1;  h = (h ^ lo32(s2_s ^ (s2_s >> 32))) * 0x85EBCA77
-//   d = mix64(rank ^ (leader_pos << 56) ^ (h << 24))
-__device__ __forceinline__ uint32_t digest_fold(uint32_t h, uint64_t s1, uint64_t s2) {
-  h = (h ^ (uint32_t)s1) * 0x9E3779B1u;
-  h = (h ^ (uint32_t)(s2 ^ (s2 >> 32))) * 0x85EBCA77u;
-  return h;
+// Per-config digest, summed over configs mod 2^64.  A linear
+// fold of 32-bit words, each times its own constant as two 16-bit halves (one
+// v_dot2_u32_u16 per word, in any order), then the rank and the leader, then
+// the murmur3 32-bit finaliser (a bijection: a config whose fold differs
+// changes its term):
+//   h = sum over the present words w:  lo16(x_w) lo16(K_w) + hi16(x_w) hi16(K_w)   (mod 2^32)
+//     slot s (0..19):     x_{2s} = lo32(S1_s),  x_{2s+1} = lo32(S2_s ^ (S2_s >> 32))
+//     leader l, f (XK):   w = 40 + 2 (16 f + l) (+1 for the sum of squares)
+//   x = h + lo32(rank) 0x9E3779B1 + hi32(rank) 0xEBCA77 + leader_pos 0xB2AE3D   (mod 2^32)
+//   d = fmix32(x)
+// (oracle/bote_oracle.cpp config_digest restates it)
+__host__ __device__ constexpr uint32_t digest_key(uint32_t w) {
+  uint64_t z = 0x9E3779B97F4A7C15ull * (uint64_t)(w + 1);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  return (uint32_t)z | 0x00010001u;
+}
+constexpr uint32_t DIGEST_WORD_LEADER = 40;  // first leader word (XK)
+typedef unsigned short dg_u16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t digest_word(uint32_t h, uint32_t x, uint32_t k) {
+  return __builtin_amdgcn_udot2(__builtin_bit_cast(dg_u16x2, x), __builtin_bit_cast(dg_u16x2, k), h, false);
+}
+// slot s's two words (s compile-time in every caller: the constants fold)
+__device__ __forceinline__ uint32_t digest_fold(uint32_t h, uint32_t s, uint64_t s1, uint64_t s2) {
+  h = digest_word(h, (uint32_t)s1, digest_key(2 * s));
+  return digest_word(h, (uint32_t)(s2 ^ (s2 >> 32)), digest_key(2 * s + 1));
+}
+// leader l's FPaxos moments at f (0: f = 1, 1: f = 2), the extended key set
+__device__ __forceinline__ uint32_t digest_fold_leader(uint32_t h, uint32_t f, uint32_t l, uint64_t s1, uint64_t s2) {
+  return digest_fold(h, DIGEST_WORD_LEADER / 2 + 16 * f + l, s1, s2);
 }
 __device__ __forceinline__ uint64_t digest_final(uint64_t rank, uint32_t lead, uint32_t h) {
-  return mix64(rank ^ ((uint64_t)lead << 56) ^ ((uint64_t)h << 24));
-}
-// The extended key set adds a second term per config: hx folds, from 0,
-// every leader's FPaxos moments (f = 1 then 2, leaders in config order), then
-// the present slots 18, 19, 14, 15, 16, 17, 10, 11, 12, 13 (the order the
-// group kernel produces them in).
-__device__ __forceinline__ uint64_t digest_final_x(uint64_t rank, uint32_t hx) {
-  return mix64(~rank ^ ((uint64_t)hx << 24));
+  uint32_t x = h + (uint32_t)rank * 0x9E3779B1u + __umul24((uint32_t)(rank >> 32), 0xEBCA77u) + __umul24(lead, 0xB2AE3Du);
+  x ^= x >> 16;
+  x *= 0x85EBCA6Bu;
+  x ^= x >> 13;
+  x *= 0xC2B2AE35u;
+  x ^= x >> 16;
+  return x;
 }
 
 // In-LDS bitonic sort of a[0..n), n a power of two, by the whole block.

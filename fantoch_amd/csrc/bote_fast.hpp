@@ -83,7 +83,7 @@ __device__ __forceinline__ bool finish_config(const FastArgs& a, const Mom (&mom
     uint32_t h = 0;
 #pragma unroll
     for (int sl = 0; sl < NSLOT; ++sl)
-      if (QC::maxf >= 2 || (sl % 5 != SLOT_AF2 && sl % 5 != SLOT_FF2)) h = digest_fold(h, mom[sl].s1, mom[sl].s2);
+      if (QC::maxf >= 2 || (sl % 5 != SLOT_AF2 && sl % 5 != SLOT_FF2)) h = digest_fold(h, sl, mom[sl].s1, mom[sl].s2);
     digest += digest_final(rank, lead_member, h);
   }
   // ---- objective keys

@@ -360,7 +360,7 @@ __device__ __forceinline__ float u64_to_f32(uint64_t x) {
 #ifndef BOTE_GROUP_WAVES_XK
 #define BOTE_GROUP_WAVES_XK 3
 #endif
-constexpr uint32_t GROUP_XK_MAX_BD = 768;
+// (GROUP_XK_MAX_BD = 768: bote_kernels.hpp)
 // client-loop quads per iteration of the base kernels (a build knob)
 #ifndef BOTE_GROUP_UNROLL
 #define BOTE_GROUP_UNROLL 4
@@ -1005,13 +1005,12 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
               }
             Mom mom[NSLOT];
             // XK: the extended slots and every leader's FPaxos moments are
-            // folded into their own digest word as they are produced
-            // (digest_final_x: the leaders, slots 18-19, 14-17, 10-13), so
-            // none stays live to the end of the config; objectives 5..7 keep
-            // one sum each (tt1, tw2, fl1)
+            // folded into the digest (a linear fold: any order) as they are
+            // produced, so none stays live to the end of the config;
+            // objectives 5..7 keep one sum each (tt1, tw2, fl1)
             uint32_t hx = 0;
             uint32_t x_tt1 = 0, x_tw2 = 0, x_fl1 = 0;
-            auto xslot = [&](uint64_t s1, uint64_t s2) { hx = digest_fold(hx, s1, s2); };
+            auto xslot = [&](uint32_t sl, uint64_t s1, uint64_t s2) { hx = digest_fold(hx, sl, s1, s2); };
             (void)xslot;
             // ---- XK, before the client loop (so that none of it stays live
             //      through it): FPaxos all leaders (Bote::all_leaders_stats, lib.rs:129-150)
@@ -1032,7 +1031,7 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
                   const uint32_t q = f == 0 ? Q2[l] : Q3[l];
                   const uint32_t m1 = __umul24(nc, q) + c1;  // (nc, q, c1 + m1 < 2^24)
                   const uint32_t m2 = __umul24(q, c1 + m1) + c2;
-                  hx = digest_fold(hx, m1, m2);
+                  hx = digest_fold_leader(hx, f, l, m1, m2);
                   if (f == 0 && m1 < b1) {
                     b1 = m1;
                     b1s = m2;
@@ -1043,15 +1042,15 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
                   }
                 }
               }
-              xslot(b1, b1s);  // slot 18 (fl1)
-              xslot(b2, b2s);  // slot 19 (fl2)
+              xslot(18, b1, b1s);  // fl1
+              xslot(19, b2, b2s);  // fl2
               x_fl1 = (uint32_t)b1;
               // Colocated Tempo: the members' own quorum latencies (slots 14..17)
               constexpr int t2 = QT::idx(2), t3 = QT::idx(3), t4 = QT::idx(4);
-              xslot(cS1t[t2], cS2[t2]);
-              xslot(cS1t[t4], cS2[t4]);
-              xslot(cS1t[t2], cS2[t2]);
-              xslot(cS1t[t3], cS2[t3]);
+              xslot(14, cS1t[t2], cS2[t2]);  // ttC1
+              xslot(15, cS1t[t4], cS2[t4]);  // ttC2
+              xslot(16, cS1t[t2], cS2[t2]);  // twC1
+              xslot(17, cS1t[t3], cS2[t3]);  // twC2
             }
             // ---- Input leaderless: 3 lane columns + the wave's nearest-fixed line
             {
@@ -1327,10 +1326,10 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
               if constexpr (XK) {
                 // Tempo tiny (2f) and write (f + 1) quorums, Input: slots 10..13
                 constexpr int t2 = QT::idx(2), t3 = QT::idx(3), t4 = QT::idx(4);
-                xslot(S1[t2], S2[t2]);  // slot 10 (tt1)
-                xslot(S1[t4], S2[t4]);  // slot 11 (tt2)
-                xslot(S1[t2], S2[t2]);  // slot 12 (tw1)
-                xslot(S1[t3], S2[t3]);  // slot 13 (tw2)
+                xslot(10, S1[t2], S2[t2]);  // tt1
+                xslot(11, S1[t4], S2[t4]);  // tt2
+                xslot(12, S1[t2], S2[t2]);  // tw1
+                xslot(13, S1[t3], S2[t3]);  // tw2
                 x_tt1 = S1[t2];
                 x_tw2 = S1[t3];
               }
@@ -1456,11 +1455,10 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
               } else {
                 if (valid) ++valid_cnt;
                 if ((SI || a.want_digest) && !ABLATE(a, 16)) {
-                  uint32_t h = 0;
+                  uint32_t h = hx;  // (0 without XK)
 #pragma unroll
-                  for (int sl = 0; sl < NSLOT; ++sl) h = digest_fold(h, mom[sl].s1, mom[sl].s2);
+                  for (int sl = 0; sl < NSLOT; ++sl) h = digest_fold(h, sl, mom[sl].s1, mom[sl].s2);
                   digest += digest_final(rank, bi, h);
-                  if constexpr (XK) digest += digest_final_x(rank, hx);
                 }
                 // ---- default objectives: 0 SCORE, 1 MEAN af1, 2 MEAN ff1, 3 COV af1, 4 MEAN e
                 if (ABLATE(a, 2048)) valid = false;

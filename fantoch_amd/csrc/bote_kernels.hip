@@ -484,23 +484,19 @@ __global__ void __launch_bounds__(256) eval_kernel(EvalArgs a) {
           uint32_t h = 0;
 #pragma unroll
           for (int sl = 0; sl < NSLOT; ++sl)
-            if (slot_has<N>(sl)) h = digest_fold(h, r.mom[sl].s1, r.mom[sl].s2);
-          digest += digest_final(rank, r.lead_orig, h);
-          if constexpr (X) {
-            // (the order of digest_final_x: all leaders, 18-19, 14-17, 10-13)
-            uint32_t hx = 0;
+            if (slot_has<N>(sl)) h = digest_fold(h, sl, r.mom[sl].s1, r.mom[sl].s2);
+          if constexpr (X) {  // the extended key set: every leader, then slots 10..19
 #pragma unroll
             for (int f = 0; f < 2; ++f) {
               if (f >= QCfg<N>::maxf) break;
 #pragma unroll
-              for (int l = 0; l < N; ++l) hx = digest_fold(hx, r.al[f][l].s1, r.al[f][l].s2);
+              for (int l = 0; l < N; ++l) h = digest_fold_leader(h, f, l, r.al[f][l].s1, r.al[f][l].s2);
             }
-            constexpr int order[10] = {18, 19, 14, 15, 16, 17, 10, 11, 12, 13};
 #pragma unroll
-            for (int i = 0; i < 10; ++i)
-              if (slot_has<N>(order[i])) hx = digest_fold(hx, r.mom[order[i]].s1, r.mom[order[i]].s2);
-            digest += digest_final_x(rank, hx);
+            for (int sl = 10; sl < 20; ++sl)
+              if (slot_has<N>(sl)) h = digest_fold(h, sl, r.mom[sl].s1, r.mom[sl].s2);
           }
+          digest += digest_final(rank, r.lead_orig, h);
         }
         if (FULL) {
           const uint64_t oi = rank - a.rb;

@@ -185,7 +185,11 @@ int fast_occupancy(uint32_t n, size_t shm);
 hipError_t launch_fast(const FastArgs& a, uint32_t n, uint32_t grid, size_t shm, hipStream_t st);
 size_t group_smem_bytes(const FastArgs& a, uint32_t n);
 bool group_uses_lines(uint32_t n);  // n <= 7: client lines (FastArgs::gslots) and register lookups
-bool group_supports_keys(uint32_t n, uint32_t bd);  // the extended key set on the group kernel (n = 4..7, bd <= 256)
+// the extended key set's group kernels are bounded to this workgroup size (3
+// waves per SIMD at <= 168 VGPRs; bote_group.hip); the capi's eligibility
+// probe and its geometry loop share it
+constexpr uint32_t GROUP_XK_MAX_BD = 768;
+bool group_supports_keys(uint32_t n, uint32_t bd);  // the extended key set on the group kernel (n = 4..7, bd <= GROUP_XK_MAX_BD)
 // workgroups per CU of the kernel instantiation launch_group runs for `a`
 // (workgroup size a.gbd)
 int group_occupancy(const FastArgs& a, uint32_t n, size_t shm, bool def_objectives);

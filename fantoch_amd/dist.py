@@ -84,42 +84,48 @@ def sharded_sweep_start(sweep, stream=None, group=None, device=None, host=None) 
     rank = dist.get_rank(group) if dist.is_initialized() else 0
     b, e = shard_of(sweep, world, rank)
     device = _device_of(sweep, device)
-    if stream is None and device.type == "cuda":
-        stream = torch.cuda.current_stream(device).cuda_stream
-    sweep.launch(b, e, stream)
-    nbytes = sweep.result_bytes()
-    if world == 1 and device.type == "cuda":
-        # one rank: the result block straight to pinned host memory
+    if device.type != "cuda":
+        sweep.launch(b, e, stream)
+        blk = torch.empty(sweep.result_bytes(), dtype=torch.uint8, device=device)
+        sweep.result_device(blk.data_ptr(), stream)
+        if world > 1:
+            gathered = torch.empty(world * blk.numel(), dtype=torch.uint8, device=device)
+            dist.all_gather_into_tensor(gathered, blk, group=group)
+            blk = merge_gathered_device(sweep, gathered, world, stream, device)
+        return PendingSweep(sweep, blk, None)
+    # Every torch operation below runs with `stream` current: the caching
+    # allocator then ties the block, the gather buffer and the merge
+    # temporaries to that stream (no reuse while it may still read them), and
+    # the collective is ordered after the sweep's writes on it.
+    cur = torch.cuda.current_stream(device)
+    if stream in (None, 0, cur.cuda_stream):
+        st, stream = cur, cur.cuda_stream
+    else:
+        st = torch.cuda.ExternalStream(stream, device=device)
+    with torch.cuda.stream(st):
+        sweep.launch(b, e, stream)
+        nbytes = sweep.result_bytes()
         if host is None:
             host = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
-        sweep.result_device(host.data_ptr(), stream)
-        ev = torch.cuda.Event()
-        cur = torch.cuda.current_stream(device)
-        ev.record(cur if stream in (None, 0, cur.cuda_stream) else torch.cuda.ExternalStream(stream, device=device))
-        return PendingSweep(sweep, host, ev)
-    blk = torch.empty(nbytes, dtype=torch.uint8, device=device)
-    sweep.result_device(blk.data_ptr(), stream)
-    if world > 1:
-        if device.type == "cuda" and dist.get_backend(group) == "gloo":
-            # gloo moves host memory: gather through the host (a rehearsal of
-            # the N-rank path with several ranks on one GPU; RCCL gathers on the device)
-            g = torch.empty(world * nbytes, dtype=torch.uint8)
-            dist.all_gather_into_tensor(g, blk.cpu(), group=group)
-            gathered = g.to(device)
+        if world == 1:
+            # one rank: the result block straight to pinned host memory
+            sweep.result_device(host.data_ptr(), stream)
         else:
-            gathered = torch.empty(world * nbytes, dtype=torch.uint8, device=device)
-            dist.all_gather_into_tensor(gathered, blk, group=group)
-        blk = merge_gathered_device(sweep, gathered, world, stream, device)
-    if device.type != "cuda":
-        return PendingSweep(sweep, blk, None)
-    if host is None:
-        host = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
-    cur = torch.cuda.current_stream(device)
-    st = cur if stream in (None, 0, cur.cuda_stream) else torch.cuda.ExternalStream(stream, device=device)
-    with torch.cuda.stream(st):
-        host.copy_(blk, non_blocking=True)
+            blk = torch.empty(nbytes, dtype=torch.uint8, device=device)
+            sweep.result_device(blk.data_ptr(), stream)
+            if dist.get_backend(group) == "gloo":
+                # gloo moves host memory: gather through the host (a rehearsal of
+                # the N-rank path with several ranks on one GPU; RCCL gathers on the device)
+                g = torch.empty(world * nbytes, dtype=torch.uint8)
+                dist.all_gather_into_tensor(g, blk.cpu(), group=group)
+                gathered = g.to(device, non_blocking=False)
+            else:
+                gathered = torch.empty(world * nbytes, dtype=torch.uint8, device=device)
+                dist.all_gather_into_tensor(gathered, blk, group=group)
+            blk = merge_gathered_device(sweep, gathered, world, stream, device)
+            host.copy_(blk, non_blocking=True)
         ev = torch.cuda.Event()
-        ev.record()
+        ev.record(st)
     return PendingSweep(sweep, host, ev)
 
 

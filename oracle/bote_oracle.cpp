@@ -553,36 +553,45 @@ uint64_t mix64(uint64_t z) {
   z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
   return z ^ (z >> 31);
 }
-// Order-independent per-config digest shared with the GPU path (DESIGN.md
-// "Digest"): a 32-bit fold of every present slot's exact sum and sum of
-// squares, then one mix64 with the rank and the leader position.
-// With the extended key set (compute_stats_x) a second term is added: hx
-// folds, from 0, every leader's FPaxos histogram (f = 1, then f = 2; leaders
-// in config order), then the present slots 18, 19, 14, 15, 16, 17, 10, 11,
-// 12, 13; the term is mix64(~rank ^ (hx << 24)).
+// Order-independent per-config digest shared with the GPU path (DESIGN.md §7,
+// fantoch_amd/csrc/bote_device.hpp digest_*), summed over configs mod 2^64:
+// a linear fold of 32-bit words, word w times its constant K_w as two 16-bit
+// halves (mod 2^32) -- slot s's exact sum (w = 2s) and sum of squares (w =
+// 2s + 1, folded to 32 bits as lo32(S2 ^ S2 >> 32)); with the extended key
+// set (compute_stats_x) also slots 10..19 and every leader's FPaxos
+// histogram (leader l at f: w = 40 + 2 (16 f + l)) -- then the rank and the
+// leader position, through the murmur3 32-bit finaliser.
+uint32_t digest_key(uint32_t w) {
+  uint64_t z = 0x9E3779B97F4A7C15ull * (uint64_t)(w + 1);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  return (uint32_t)z | 0x00010001u;
+}
+uint32_t digest_word(uint32_t h, uint32_t x, uint32_t k) {
+  return h + (x & 0xFFFFu) * (k & 0xFFFFu) + (x >> 16) * (k >> 16);
+}
 uint64_t config_digest(uint64_t rank, const ProtocolStats& st) {
-  auto fold = [](uint32_t h, const Histogram& hh) {
+  auto fold = [](uint32_t h, uint32_t s, const Histogram& hh) {
     uint64_t s1, c;
     hh.sum_and_count(s1, c);
     uint64_t s2 = hh.sumsq();
-    h = (h ^ (uint32_t)s1) * 0x9E3779B1u;
-    h = (h ^ (uint32_t)(s2 ^ (s2 >> 32))) * 0x85EBCA77u;
-    return h;
+    h = digest_word(h, (uint32_t)s1, digest_key(2 * s));
+    return digest_word(h, (uint32_t)(s2 ^ (s2 >> 32)), digest_key(2 * s + 1));
   };
   uint32_t h = 0;
-  for (int s = 0; s < NKEYS; ++s)
-    if (st.has[s]) h = fold(h, st.h[s]);
-  uint64_t d = mix64(rank ^ ((uint64_t)st.leader_pos << 56) ^ ((uint64_t)h << 24));
-  if (!st.all_leaders[0].empty()) {  // the extended key set
-    uint32_t hx = 0;
-    for (int f = 0; f < 2; ++f)
-      for (auto& hh : st.all_leaders[f]) hx = fold(hx, hh);
-    static const int order[10] = {18, 19, 14, 15, 16, 17, 10, 11, 12, 13};
-    for (int s : order)
-      if (st.has[s]) hx = fold(hx, st.h[s]);
-    d += mix64(~rank ^ ((uint64_t)hx << 24));
-  }
-  return d;
+  for (int s = 0; s < NKEYS_X; ++s)
+    if (st.has[s]) h = fold(h, (uint32_t)s, st.h[s]);
+  for (int f = 0; f < 2; ++f)  // (empty unless the extended key set)
+    for (size_t l = 0; l < st.all_leaders[f].size(); ++l) h = fold(h, 20 + 16 * f + (uint32_t)l, st.all_leaders[f][l]);
+  uint32_t x = h + (uint32_t)rank * 0x9E3779B1u + (uint32_t)(rank >> 32) * 0xEBCA77u +
+               (uint32_t)st.leader_pos * 0xB2AE3Du;
+  x ^= x >> 16;
+  x *= 0x85EBCA6Bu;
+  x ^= x >> 13;
+  x *= 0xC2B2AE35u;
+  x ^= x >> 16;
+  return x;
 }
 
 thread_local std::string g_err;

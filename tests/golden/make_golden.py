@@ -2,7 +2,7 @@
 oracle (oracle/bote_oracle.cpp, itself pinned to the reference's own
 known-answer tests in reference_goldens.json by tests/test_oracle.py).
 
-  python tests/golden/make_golden.py
+  python tests/golden/make_golden.py [topk]     (topk: only topk.json)
 
 Writes:
   planets.npz            parsed GCP, AWS 2020_06_05 and AWS 2021_02_13
@@ -66,6 +66,13 @@ def main():
     gcp = Planet.new()
     aws20 = Planet.from_dir(AWS_2020_DIR)
     aws21 = Planet.from_dir(AWS_2021_DIR)
+    only_topk = sys.argv[1:] == ["topk"]
+    if not only_topk:
+        write_stats(gcp, aws20, aws21)
+    write_topk(gcp, aws21)
+
+
+def write_stats(gcp, aws20, aws21):
     np.savez_compressed(os.path.join(HERE, "planets.npz"),
                         gcp_lat=gcp.lat.astype(np.uint16), gcp_names=np.array(gcp.names),
                         aws20_lat=aws20.lat.astype(np.uint16), aws20_names=np.array(aws20.names),
@@ -88,6 +95,8 @@ def main():
         out[f"n{n}_sample_vals"] = vals[::SAMPLE_EVERY].astype(np.uint16)
     np.savez_compressed(os.path.join(HERE, "gcp_n3_n5_stats.npz"), **out)
 
+
+def write_topk(gcp, aws21):
     topk = {"_doc": "oracle top-K (key, colex rank) per objective; objectives = DEFAULT_OBJECTIVES "
                     "(kind, slot); RankingParams(110,35,0,15,F1F2); K=%d" % TOPK_K,
             "objectives": [list(x) for x in DEFAULT_OBJECTIVES], "K": TOPK_K, "cases": {}}

@@ -11,10 +11,14 @@ Writes:
                 sub-ranges of topk.json, swept with the extended key set:
                 valid count, digest and top-K (K=32) of the config-5
                 objectives (bote.CONFIG5_OBJECTIVES; n < 4: tw1 for tw2)
-  syn_r128n6_windows.json  (appends) 64 windows of 10^5 ranks at seeded
-                random offsets of [0, C(128, 6)), each swept with the base
-                key set (the 10 compute_stats keys, DEFAULT_OBJECTIVES, K=100)
-                and with the extended one (CONFIG5_OBJECTIVES): "random": true
+  syn_r128n6_windows.json  nine 10^6-rank windows, eight of them straddling
+                a colex boundary C(m, 6) where every member changes (base key
+                set: the 10 compute_stats keys, DEFAULT_OBJECTIVES, K=100);
+                256 windows at seeded random offsets of [0, C(128, 6)),
+                "random": true -- the first 64 draws of 10^5 ranks, each swept
+                with the base key set and with the extended one
+                (CONFIG5_OBJECTIVES, under "x"), the other 192 of 2.5 10^4
+                ranks with the extended key set only ("x_only": true)
 Resumable: finished windows are kept in oracle/build/keys_windows.jsonl.
 
 Data only: inputs and expected outputs.
@@ -41,7 +45,10 @@ from fantoch_amd.planet import Planet  # noqa: E402
 RP = (110.0, 35.0, 0.0, 15.0)
 K_TOPK = 32
 SYN = {"r64n7": (64, 7, 310_608_096, 60_000), "r128n6": (128, 6, 2_711_805_600, 40_000)}
-N_WINDOWS, WIN = 64, 100_000
+N_WINDOWS, WIN = 64, 100_000  # random windows with both key sets
+N_WINDOWS_X, WIN_X = 192, 25_000  # more random windows, extended key set only
+BOUNDARY = (0, 3338380, 49563860, 300000200, 1191552400, 2141351635, 3652245460, 5168879425, 5422611200)
+WIN_B = 1_000_000
 SEED = 0x5EED0128
 
 
@@ -77,10 +84,13 @@ def make_topk(threads):
     json.dump(out, open(os.path.join(HERE, "topk_x.json"), "w"), indent=0)
 
 
-def window_begins():
+def window_begins(x_only=False):
+    """The first N_WINDOWS draws (both key sets), or the next N_WINDOWS_X (the
+    extended key set only), of one seeded stream."""
     total = comb(128, 6)
     rng = np.random.default_rng(SEED)
-    return sorted(int(x) for x in rng.integers(0, total - WIN, size=N_WINDOWS))
+    b = [int(x) for x in rng.integers(0, total - WIN, size=N_WINDOWS + N_WINDOWS_X)]
+    return sorted(b[N_WINDOWS:]) if x_only else sorted(b[:N_WINDOWS])
 
 
 def make_windows(threads):
@@ -91,66 +101,49 @@ def make_windows(threads):
     if os.path.exists(scratch):
         for line in open(scratch):
             w = json.loads(line)
-            done[w["rank_begin"]] = w
-    for b in window_begins():
-        if b in done:
+            done[(w["rank_begin"], w.get("kind"))] = w
+    jobs = [("boundary", b, WIN_B) for b in BOUNDARY] + [("random", b, WIN) for b in window_begins()] + \
+           [("random_x", b, WIN_X) for b in window_begins(x_only=True)]
+    for kind, b, win in jobs:
+        if (b, kind) in done:
             continue
         t0 = time.time()
-        base = sweep_case(p, 6, b, b + WIN, DEFAULT_OBJECTIVES, 100, 0, threads)
-        x = sweep_case(p, 6, b, b + WIN, objectives_x(6), 100, 1, threads)
-        w = dict(R=128, n=6, rank_begin=b, rank_end=b + WIN, K=100, random=True,
-                 objectives=[list(o) for o in DEFAULT_OBJECTIVES], ranking=list(RP), ft_metric=2, **base,
-                 x=dict(keys=1, objectives=[list(o) for o in objectives_x(6)], **x),
-                 cpu_seconds_wall=round(time.time() - t0, 1), threads=threads)
+        w = dict(R=128, n=6, rank_begin=b, rank_end=b + win, K=100, kind=kind)
+        if kind != "random_x":
+            base = sweep_case(p, 6, b, b + win, DEFAULT_OBJECTIVES, 100, 0, threads)
+            w.update(objectives=[list(o) for o in DEFAULT_OBJECTIVES], ranking=list(RP), ft_metric=2, **base)
+        if kind != "boundary":
+            x = sweep_case(p, 6, b, b + win, objectives_x(6), 100, 1, threads)
+            w["random"] = True
+            w["valid"] = x.pop("valid")
+            w["x"] = dict(keys=1, objectives=[list(o) for o in objectives_x(6)], ranking=list(RP), ft_metric=2, **x)
+        if kind == "random_x":
+            w["x_only"] = True
+        w.update(cpu_seconds_wall=round(time.time() - t0, 1), threads=threads)
         with open(scratch, "a") as fh:
             fh.write(json.dumps(w) + "\n")
-        done[b] = w
-        print("window", b, len(done), "/", N_WINDOWS, round(time.time() - t0, 1), "s", flush=True)
+        done[(b, kind)] = w
+        print("window", kind, b, len(done), "/", len(jobs), round(time.time() - t0, 1), "s", flush=True)
     path = os.path.join(HERE, "syn_r128n6_windows.json")
-    d = json.load(open(path))
-    keep = [w for w in d["windows"] if not w.get("random")]
-    d["windows"] = keep + [done[b] for b in window_begins()]
-    d["what"] = ("oracle sweeps of windows of the synthetic R=128 planet, n=6: nine 10^6-rank windows (eight "
-                 "straddling a colex boundary C(m, 6)) and 64 10^5-rank windows at seeded random offsets "
-                 "(\"random\": true, also swept with the extended key set under \"x\")")
-    d["generator"] = "scripts/oracle_fixtures.sh; tests/golden/make_keys_golden.py (random windows)"
+    d = {"what": ("oracle sweeps of windows of the synthetic R=128 planet, n=6: nine 10^6-rank windows (eight "
+                  "straddling a colex boundary C(m, 6)), 64 10^5-rank windows at seeded random offsets "
+                  "(\"random\": true, also swept with the extended key set under \"x\") and 192 2.5 10^4-rank "
+                  "windows at further seeded random offsets swept with the extended key set only "
+                  "(\"x_only\": true)"),
+         "generator": "tests/golden/make_keys_golden.py windows",
+         "windows": [done[(b, k)] for k, b, _ in jobs]}
     json.dump(d, open(path, "w"))
 
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("what", nargs="?", default="all", choices=["topk", "windows", "all", "refresh_x"])
+    ap.add_argument("what", nargs="?", default="all", choices=["topk", "windows", "all"])
     ap.add_argument("--threads", type=int, default=8)
     a = ap.parse_args()
     if a.what in ("topk", "all"):
         make_topk(a.threads)
     if a.what in ("windows", "all"):
         make_windows(a.threads)
-    if a.what == "refresh_x":
-        make_topk(a.threads)
-        refresh_x(a.threads)
-
-
-
-def refresh_x(threads):
-    """Recompute the extended-key part of every fixture with the current
-    oracle and rewrite the entries that differ (used once after the digest's
-    definition changed while a generation was running)."""
-    p = Planet.synthetic(128)
-    path = os.path.join(HERE, "syn_r128n6_windows.json")
-    d = json.load(open(path))
-    changed = 0
-    for w in d["windows"]:
-        if "x" not in w:
-            continue
-        b, e = w["rank_begin"], w["rank_end"]
-        x = sweep_case(p, 6, b, e, objectives_x(6), 100, 1, threads)
-        if (x["valid"], x["digest"], x["tops"]) != (w["valid"], w["x"]["digest"], w["x"]["tops"]):
-            w["x"].update(digest=x["digest"], tops=x["tops"])
-            changed += 1
-        print("window", b, "x", "changed" if changed else "same", flush=True)
-    json.dump(d, open(path, "w"))
-    print("windows refreshed:", changed)
 
 
 if __name__ == "__main__":

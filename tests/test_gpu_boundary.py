@@ -92,7 +92,13 @@ def test_search_handle_repeated_launch_is_device_work_only():
           f"single sweep {t_single * 1e3:.2f} ms; ratio {t_handle / t_single:.3f}")
     r = h.result()
     assert (r.valid, r.digest, r.tops) == want
-    assert t_handle < 1.25 * t_single
+    assert t_handle < 1.15 * t_single
+    # back-to-back launches with no result() between them: the second launch's
+    # shard copies wait for the first launch's merge tree (bote_search::merged_ev)
+    for _ in range(3):
+        h.launch()
+    r = h.result()
+    assert (r.valid, r.digest, r.tops) == want
 
 
 def test_search_handle_errors_leave_no_state():

@@ -58,7 +58,7 @@ def test_moments_x_equal_single_calls(planet, n):
 
 def test_sweep_x_keeps_base_results_and_changes_digest():
     """The extended key set leaves valid counts and the compute_stats objectives
-    unchanged; its digest adds the second term."""
+    unchanged; its digest also folds the extended slots and every leader."""
     p = Planet.new()
     o = O.OraclePlanet.of(p)
     s = np.arange(p.R, dtype=np.uint32)
@@ -67,3 +67,61 @@ def test_sweep_x_keeps_base_results_and_changes_digest():
     t1, v1, d1 = o.sweep(s, s, 5, 0, 15504, objs + [(1, 10), (1, 13), (1, 18)], 16, threads=4, keys=1)
     assert v0 == v1 and t1[:5] == t0 and d0 != d1
     assert all(len(t) == 16 for t in t1)
+
+
+def _digest_key(w):
+    M = (1 << 64) - 1
+    z = (0x9E3779B97F4A7C15 * (w + 1)) & M
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & M
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & M
+    z ^= z >> 31
+    return (z & 0xFFFFFFFF) | 0x00010001
+
+
+def _digest(rank, lead, words):
+    """DESIGN.md §7, written out: words = [(w, 32-bit value)]."""
+    h = 0
+    for w, x in words:
+        k = _digest_key(w)
+        h = (h + (x & 0xFFFF) * (k & 0xFFFF) + (x >> 16) * (k >> 16)) & 0xFFFFFFFF
+    x = (h + (rank & 0xFFFFFFFF) * 0x9E3779B1 + (rank >> 32) * 0xEBCA77 + lead * 0xB2AE3D) & 0xFFFFFFFF
+    x ^= x >> 16
+    x = (x * 0x85EBCA6B) & 0xFFFFFFFF
+    x ^= x >> 13
+    x = (x * 0xC2B2AE35) & 0xFFFFFFFF
+    return x ^ (x >> 16)
+
+
+@pytest.mark.parametrize("planet,n,keys", [("gcp", 3, 0), ("gcp", 5, 0), ("gcp", 5, 1), ("gcp", 2, 1),
+                                           ("syn128", 6, 1), ("syn128", 6, 0)])
+def test_sweep_digest_is_the_written_definition(planet, n, keys):
+    """The oracle sweep's digest (the certificate every device sweep is checked
+    against) equals DESIGN.md §7's formula applied to the oracle's own
+    per-config moments: slot s's sum at word 2s and its folded sum of squares
+    at 2s + 1, every leader of the extended key set at 40 + 2 (16 f + l)."""
+    p = Planet.new() if planet == "gcp" else Planet.synthetic(128)
+    o = O.OraclePlanet.of(p)
+    s = np.arange(p.R, dtype=np.uint32)
+    rb = 0 if planet == "gcp" else 2_711_805_600
+    re = rb + min(600, _lib.binomial(p.R, n))
+    _, _, dig = o.sweep(s, s, n, rb, re, [(1, 0)], 4, threads=2, keys=keys)
+    cfgs = np.array([O.colex_unrank(r, n, p.R) for r in range(rb, re)], dtype=np.uint32)
+    s1, s2, a1, a2, lead = o.moments_x(cfgs, s, threads=2)
+    none = np.iinfo(np.uint64).max
+    mf = min(n // 2, 2)
+    want = 0
+    for i, r in enumerate(range(rb, re)):
+        words = []
+        for sl in range(20 if keys else 10):
+            if s1[i, sl] == none:
+                continue
+            q = int(s2[i, sl])
+            words += [(2 * sl, int(s1[i, sl]) & 0xFFFFFFFF), (2 * sl + 1, (q ^ (q >> 32)) & 0xFFFFFFFF)]
+        if keys:
+            for f in range(mf):
+                for l in range(n):
+                    q = int(a2[i, f, l])
+                    w = 40 + 2 * (16 * f + l)
+                    words += [(w, int(a1[i, f, l]) & 0xFFFFFFFF), (w + 1, (q ^ (q >> 32)) & 0xFFFFFFFF)]
+        want += _digest(r, int(lead[i]), words)
+    assert dig == want % (1 << 64)

@@ -67,3 +67,20 @@ def test_bench_refuses_world_not_equal_to_gpus():
     r = _bench(["--gpus", "4", "--steps", "1", "--warmup", "0", "--no-cpu-baseline"],
                {"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
     assert r.returncode != 0 and "!= --gpus 4" in r.stderr, r.stderr
+
+
+def test_launcher_retries_a_taken_rendezvous_port(tmp_path):
+    """A world whose rank exits PORT_IN_USE (its rendezvous port was taken) is
+    started again on a new port; other failures are not retried."""
+    sys.path.insert(0, ROOT)
+    from fantoch_amd.launch import PORT_IN_USE, run_world
+
+    marker = tmp_path / "tried"
+    script = tmp_path / "port_once.py"
+    script.write_text("import os, pathlib, sys\n"
+                      f"tried = list(pathlib.Path({str(tmp_path)!r}).glob('tried*'))\n"
+                      f"pathlib.Path({str(marker)!r} + str(len(tried))).write_text(os.environ['MASTER_PORT'])\n"
+                      f"sys.exit({PORT_IN_USE} if len(tried) == 0 and os.environ['RANK'] == '0' else 0)\n")
+    assert run_world(1, [str(script)], timeout=60) == 0
+    assert len(list(tmp_path.glob("tried*"))) == 2  # two attempts, on two ports
+    assert run_world(1, [str(script)], timeout=60, port=12345) == 0  # (fixed port: marker exists, exits 0)
