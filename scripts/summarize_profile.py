@@ -1,4 +1,4 @@
-"""Summarise a scripts/gpu_profile.sh run (gpurun_out/prof/<TAG>_*) into
+"""Summarise a `STEPS=profile` run of scripts/gpu_job.sh (gpurun_out/<TAG>/trace, pmc1..4) into
 profiles/<TAG>_profile.md and update profiles/traffic.json.
 
   python scripts/summarize_profile.py r01 [workload_tag]
@@ -23,9 +23,9 @@ CONFIGS = {"r64n7": 621216192, "r128n6": 5423611200}
 def main():
     tag = sys.argv[1]
     wl = sys.argv[2] if len(sys.argv) > 2 else "r64n7_n1"
-    src = os.path.join(ROOT, "gpurun_out", "prof")
+    src = os.path.join(ROOT, "gpurun_out", tag)
     out = []
-    stats = os.path.join(src, f"{tag}_trace", "run_kernel_stats.csv")
+    stats = os.path.join(src, "trace", "run_kernel_stats.csv")
     rows = list(csv.DictReader(open(stats)))
     out.append(f"# rocprofv3 summary {tag} ({wl})\n")
     out.append("## Kernel trace (`rocprofv3 --kernel-trace --stats`)\n")
@@ -43,7 +43,7 @@ def main():
     # duration (a sample launch is < 1/4 of the longest) so that the averages
     # below describe the sweep launch alone.
     durs = collections.defaultdict(list)
-    tr = os.path.join(src, f"{tag}_trace", "run_kernel_trace.csv")
+    tr = os.path.join(src, "trace", "run_kernel_trace.csv")
     if os.path.exists(tr):
         for r in csv.DictReader(open(tr)):
             durs[r["Kernel_Name"]].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
@@ -58,8 +58,8 @@ def main():
     counters = collections.defaultdict(lambda: collections.defaultdict(float))
     ndisp = collections.defaultdict(set)
     i = 1
-    while os.path.exists(os.path.join(src, f"{tag}_pmc{i}", "run_counter_collection.csv")):
-        rows_i = list(csv.DictReader(open(os.path.join(src, f"{tag}_pmc{i}", "run_counter_collection.csv"))))
+    while os.path.exists(os.path.join(src, f"pmc{i}", "run_counter_collection.csv")):
+        rows_i = list(csv.DictReader(open(os.path.join(src, f"pmc{i}", "run_counter_collection.csv"))))
         longest = collections.defaultdict(int)
         for r in rows_i:
             longest[r["Kernel_Name"]] = max(longest[r["Kernel_Name"]],
