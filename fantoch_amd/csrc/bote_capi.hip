@@ -144,6 +144,7 @@ struct bote_sweep {
   uint32_t xgrid = 0;  // generic fixup grid (deferred configs)
   DBuf cqt, rqt, queue, qcount, lowtab;
   DBuf dbg;  // BOTE_DEBUG builds: device-assert flag bits
+  DBuf pstats;  // BOTE_PATHSTATS builds: 64 path counters (group kernel)
   // group kernel work chunks per launch range (cached: a bench or a shard
   // re-launches the same range), plus the ticket counter
   struct Chunks {
@@ -763,6 +764,7 @@ int bote_sweep_create_keys(const bote_planet* p, const uint32_t* servers, uint32
   // (latency << 4 | member) below 2^24 and two squared keys below 2^32,
   // bote_group.hip)
   const bool keys32 = (uint64_t)nc * (2 * maxlat_all) * (2 * maxlat_all) < (1ull << 32) &&
+                      (uint64_t)nc * maxlat_all < (1ull << 16) &&  // (packed member-pair bins)
                       3ull * nc * maxlat_all < (1ull << 24) && nc < 256 &&
                       (uint64_t)nc * (16 * maxlat_all + 15) < (1ull << 24) &&
                       2 * (16 * maxlat_all + 15) * (16 * maxlat_all + 15) < (1ull << 32);
@@ -816,7 +818,8 @@ int bote_sweep_create_keys(const bote_planet* p, const uint32_t* servers, uint32
     // every slot's sum of squares below 2^32 (a value is at most a latency
     // plus a quorum latency, 2 max, over nc >= N clients): the bench-shaped
     // group kernels keep the moments in 32 bits (bote_group.hip S32)
-    f.s32 = (uint64_t)std::max(nc, n) * amax * amax < (1ull << 32) ? 1u : 0u;
+    // (and the FPaxos moments' 24-bit multiplies: column sum + S1 <= 3 nc max < 2^24)
+    f.s32 = (uint64_t)std::max(nc, n) * amax * amax < (1ull << 32) && 3ull * nc * maxlat < (1ull << 24) ? 1u : 0u;
     f.v32 = f.s32 && (uint64_t)std::max(nc, n) * std::max(nc, n) * amax * amax < (1ull << 32) ? 1u : 0u;
     f.want_score = a.want_score;
     f.p_fmean = a.p_fmean;
@@ -850,6 +853,11 @@ int bote_sweep_create_keys(const bote_planet* p, const uint32_t* servers, uint32
     if (s->dbg.alloc(16) != hipSuccess || hipMemset(s->dbg.p, 0, 16) != hipSuccess)
       return cleanup(fail(BOTE_E_NOMEM, "debug flag"));
     f.dbg_flag = s->dbg.as<unsigned int>();
+#endif
+#ifdef BOTE_PATHSTATS
+    if (s->pstats.alloc(64 * 8) != hipSuccess || hipMemset(s->pstats.p, 0, 64 * 8) != hipSuccess)
+      return cleanup(fail(BOTE_E_NOMEM, "path counters"));
+    f.pstats = s->pstats.as<unsigned long long>();
 #endif
 #ifdef BOTE_ABLATION
     const char* abl = getenv("BOTE_ABLATE");  // timing-diagnostics builds only
@@ -897,6 +905,7 @@ int bote_sweep_create_keys(const bote_planet* p, const uint32_t* servers, uint32
       // clients, where the bin fields cannot overflow
       f.gbins = !keys && s->def_obj && bote::group_uses_lines(n) && nc >= 96 && nc < 256 && f.srv_identity &&
                 f.want_digest && f.ft_metric == 2 && (uint64_t)nc * (16ull * maxlat + 15) < (1ull << 24) &&
+                (uint64_t)nc * maxlat < (1ull << 16) &&  // (packed member-pair bins)
                 2 * (16ull * maxlat + 15) * (16ull * maxlat + 15) < (1ull << 32);
       struct GGeo {
         uint32_t bd = 0, grx = 0, gslots = 0, gqsh = 10;
@@ -1295,6 +1304,20 @@ int bote_sweep_launch(bote_sweep* s, uint64_t rank_begin, uint64_t rank_end, voi
 }
 
 uint64_t bote_sweep_result_bytes(const bote_sweep* s) { return s ? s->result_bytes() : 0; }
+
+#ifdef BOTE_PATHSTATS
+// Path-statistics builds only (not in include/bote_hip.h): the 64 group-kernel
+// path counters since the last call (read, then reset; scripts/pathstats.py).
+int bote_sweep_pathstats(bote_sweep* s, uint64_t* out) {
+  DevGuard dev_guard;
+  if (!s || !out || !s->pstats.p) return fail(BOTE_E_ARG, "no path counters");
+  HIP_TRY(hipSetDevice(s->p->device));
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpy(out, s->pstats.p, 64 * 8, hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemset(s->pstats.p, 0, 64 * 8));
+  return BOTE_OK;
+}
+#endif
 
 int bote_sweep_result_device(bote_sweep* s, void* dst, void* hip_stream) {
   DevGuard dev_guard;  // the caller's current device is restored on return

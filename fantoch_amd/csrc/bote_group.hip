@@ -495,6 +495,7 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
     if (c >= a.nwchunks) break;
     if (lane == 0) cnext = atomicAdd(tctr, 1u);
     chunk = c;
+    PSTAT(a, 13, true);  // chunks
     r = uni64(a.wchunks[c]);
     rend = a.smin ? min(r + 64ull * a.ssteps, a.re) : uni64(a.wchunks[c + 1]);  // (sample chunks: ssteps steps)
     GASSERT(a, a.rb <= r && r <= rend && rend <= a.re, 0);  // chunk inside the launch range
@@ -540,6 +541,7 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
 #endif
     for (;;) {
       const uint64_t gend = base + uni64(binom[hq[0] * (N + 1) + 3]);
+      PSTAT(a, 12, true);  // groups (precomputes)
       // ---------------- per-group, wave-uniform precompute -> group line
       uint32_t freg[F];
 #pragma unroll
@@ -620,6 +622,7 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
       while (left) {
         const uint32_t len = min(64u, left);
         bool have = lane < len;
+        PSTAT(a, 0, true);  // steps
         const uint32_t cur = lp3;
         // prefetch the next step's low part (the load overlaps this step)
         if (left > len) lp3 = a.lowtab[lo32 + len + min(lane, left - len - 1)];
@@ -642,6 +645,7 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
           const uint64_t nk = __ballot(have && ((cur & 0xFFu) == 0 || lane == 0));
           const uint32_t nsl = (uint32_t)__popcll(nk);
           use_lines = nsl <= a.gslots && !ABLATE(a, 4096);
+          PSTAT(a, 1, !use_lines);  // more distinct (p1, p2) than line slots
           if (use_lines) {
             // slot = index of the lane's pair among the step's pairs; the
             // first lane of each pair publishes its key to the wave's slot table
@@ -966,6 +970,7 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
             const float m = __uint_as_float(mu & ~IM), m2 = __uint_as_float(m2u & ~IM);
             amb = m < __builtin_inff() && m2 >= m * (1.0f - 0x1p-18f);
           }
+          PSTAT(a, 2, amb);  // leader within the f32 band: exact re-scan
           if (amb) {  // exact re-scan in the generic path's arithmetic
             amb = false;
             bi = 0;
@@ -989,6 +994,7 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
             }
           }
           GASSERT(a, bi < (uint32_t)N, 7);  // leader member
+          PSTAT(a, 3, amb);  // leader deferred
           if (amb) {
             if (!a.smin) defer_rank(a, rank);
             have = false;
@@ -1272,38 +1278,59 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
                 };
                 if (use_lines) clients_bin(BoolC<true>{});
                 else clients_bin(BoolC<false>{});
-                // the bins (re-zeroed for the next config of this lane)
-                uint32_t cnt[N], D1[N], L1 = 0;
-                uint64_t corr = 0;  // 32 sum_m m D1_m + sum_m m^2 cnt_m
+                // the bins (re-zeroed for the next config of this lane), in
+                // packed member pairs laid out as the tables' words wp[t][i]
+                // (members (0, 1), 2, (3, 4), (5, 6); a lone member's high
+                // half is don't-care: its table word's high half is 0), so
+                // each table's sums are one v_dot2 per word.  The host admits
+                // the bins only where nc max < 2^16 (bote_capi.hip), so every
+                // count, every D1_m and every cnt_m q product fits a u16.
+                constexpr int NW = 2 + FP;
+                uint32_t wv[N], hv[N];  // bin words; (K_m - m cnt_m) >> 4 = D1_m | cnt_m << 20
 #pragma unroll
                 for (int m = 0; m < N; ++m) {
-                  const uint32_t w = l32(bin + 256u * m);
+                  wv[m] = l32(bin + 256u * m);
                   s32(bin + 256u * m, 0u);
-                  cnt[m] = w >> 24;
-                  D1[m] = ((w & 0xFFFFFFu) - (uint32_t)m * cnt[m]) >> 4;
-                  L1 += D1[m];
-                  if (m) corr += (uint64_t)(32u * m) * D1[m] + (uint32_t)(m * m) * cnt[m];
+                  hv[m] = (m ? wv[m] - (uint32_t)m * (wv[m] >> 24) : wv[m]) >> 4;
+                }
+                uint32_t cW[NW], dW[NW];  // (cnt_m | cnt_m' << 16), (D1_m | D1_m' << 16)
+                constexpr int wlo[4] = {0, 2, 3, 5}, whi[4] = {1, -1, 4, 6};
+#pragma unroll
+                for (int i = 0; i < NW; ++i) {
+                  const int ml = wlo[i], mh = whi[i] < N ? whi[i] : -1;
+                  if (mh >= 0) {
+                    cW[i] = __builtin_amdgcn_perm(wv[mh], wv[ml], 0x0C070C03u);
+                    dW[i] = __builtin_amdgcn_perm(hv[mh], hv[ml], 0x05040100u);
+                  } else {
+                    cW[i] = wv[ml] >> 24;
+                    dW[i] = hv[ml];
+                  }
+                }
+                // L1 = sum_m D1_m; corr = 32 sum_m m D1_m + sum_m m^2 cnt_m
+                // (per word constant pairs; a lone member's high weight 0)
+                uint32_t L1 = 0, corr = 0;
+#pragma unroll
+                for (int i = 0; i < NW; ++i) {
+                  const int ml = wlo[i], mh = whi[i] < N ? whi[i] : -1;
+                  const uint32_t one = mh >= 0 ? 0x00010001u : 1u;
+                  const uint32_t k32 = (uint32_t)(32 * ml) | (mh >= 0 ? (uint32_t)(32 * mh) << 16 : 0u);
+                  const uint32_t kmm = (uint32_t)(ml * ml) | (mh >= 0 ? (uint32_t)(mh * mh) << 16 : 0u);
+                  L1 = __builtin_amdgcn_udot2(as_us2(dW[i]), as_us2(one), L1, false);
+                  corr = __builtin_amdgcn_udot2(as_us2(dW[i]), as_us2(k32), corr, false);
+                  corr = __builtin_amdgcn_udot2(as_us2(cW[i]), as_us2(kmm), corr, false);
                 }
                 L2 = (L2 - corr) >> 8;  // exact: the sum of squared keys is 256 L2 + corr
 #pragma unroll
                 for (int t = 0; t < NT; ++t) {
-                  // member m's quorum latency in table t (wp: the packed rows)
-                  uint32_t qv[N];
-                  qv[0] = wp[t][0] & 0xFFFFu;
-                  qv[1] = wp[t][0] >> 16;
-                  qv[2] = wp[t][1] & 0xFFFFu;
-#pragma unroll
-                  for (int m = 3; m < N; ++m) {
-                    const uint32_t w = wp[t][2 + (m - 3) / 2];
-                    qv[m] = ((m - 3) & 1) ? w >> 16 : w & 0xFFFFu;
-                  }
+                  // S1 = L1 + sum cnt q;  S2 = L2 + 2 sum D1 q + sum (cnt q) q
                   uint32_t s1 = L1, x = 0, qq = 0;
 #pragma unroll
-                  for (int m = 0; m < N; ++m) {
-                    const uint32_t cq = __umul24(cnt[m], qv[m]);
-                    s1 += cq;
-                    qq = __umul24(cq, qv[m]) + qq;
-                    x = __umul24(D1[m], qv[m]) + x;
+                  for (int i = 0; i < NW; ++i) {
+                    const us2 q = as_us2(wp[t][i]);
+                    s1 = __builtin_amdgcn_udot2(as_us2(cW[i]), q, s1, false);
+                    x = __builtin_amdgcn_udot2(as_us2(dW[i]), q, x, false);
+                    const us2 cq = as_us2(cW[i]) * q;  // (v_pk_mul_lo_u16: cnt q < 2^16)
+                    qq = __builtin_amdgcn_udot2(cq, q, qq, false);
                   }
                   S1[t] = s1;
                   S2[t] = L2 + ((uint64_t)x << 1) + qq;
@@ -1337,11 +1364,12 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
             // ---- Input FPaxos from the leader column's sums
             const uint32_t lc1 = lrec[lpos].x;
             if constexpr (S32) {
-              // sum (L + q) and sum (L + q)^2 = c2 + q (c1 + S1), in 32 bits
+              // sum (L + q) and sum (L + q)^2 = c2 + q (c1 + S1), in 32 bits,
+              // with 24-bit multiplies (FastArgs::s32: c1 + S1 <= 3 nc max < 2^24)
               const uint32_t lc2 = (uint32_t)cs2[lpos];
               const uint32_t m2 = __umul24(nc, lq2) + lc1, m3 = __umul24(nc, lq3) + lc1;
-              mom[SLOT_FF1] = Mom{m2, (uint32_t)(lq2 * (lc1 + m2) + lc2), nc};
-              mom[SLOT_FF2] = Mom{m3, (uint32_t)(lq3 * (lc1 + m3) + lc2), nc};
+              mom[SLOT_FF1] = Mom{m2, __umul24(lq2, lc1 + m2) + lc2, nc};
+              mom[SLOT_FF2] = Mom{m3, __umul24(lq3, lc1 + m3) + lc2, nc};
             } else {
               const uint64_t lc2 = cs2[lpos];
               mom[SLOT_FF1] = leader_mom(lc1, lc2, nc, lq2);
@@ -1419,6 +1447,7 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
                   // [m1_lo, m1_hi], by the reference's f64 arithmetic inside
                   const int32_t D = (int32_t)((uint32_t)mf.s1 - (uint32_t)ma.s1);
                   bool mok = D > a.m1_hi;
+                  PSTAT(a, 4 + f - 1, D >= a.m1_lo && D <= a.m1_hi);  // f64 mean test (f = 1, 2)
                   if (D >= a.m1_lo && D <= a.m1_hi) mok = (mom_mean(mf) - mom_mean(ma)) >= a.p_fmean;
                   valid = valid && mok;
                   if (N == 11 || N == 13) {
@@ -1428,6 +1457,7 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
                     valid = valid && eok;
                   }
                 }
+                PSTAT(a, 6, valid);  // COV validity tests
                 if (valid) {
                   // cov_f >= cov_a (min_fairness_fpaxos_improv == 0 on this path):
                   // cross-multiplied f32 screen, then f64 (cov2_sign)
@@ -1450,6 +1480,7 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
                   defer = !lt && amb_c;
                 }
               }
+              PSTAT(a, 8, defer);  // validity deferred
               if (defer) {
                 if (!a.smin) defer_rank(a, rank);
               } else {
@@ -1490,6 +1521,7 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
                     }
                     maybe = !(tscore == tscore) || (double)T >= (tscore - 1e-6) * (double)nc;
                   }
+                  PSTAT(a, 9, maybe);  // f64 score
                   if (maybe) {
                     double score = 0.0;
                     const double me = mom_mean(mom[SLOT_E]);
@@ -1517,6 +1549,7 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
                     const float S = (float)(uint32_t)m.s1;
                     maybe = va1 <= (float)__longlong_as_double((long long)tk3) * (S * S) * (1.0f + 0x1p-10f);
                   }
+                  PSTAT(a, 10, maybe);  // COV af1 key (f64)
                   if (maybe) {
                     ok[3] = true;
                     key[3] = cov_key(m);
@@ -1551,6 +1584,7 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
 #pragma unroll
           for (int o = 0; o < MAXOBJ; ++o)
             if (o < nobj) pass = pass || (ok[o] && key[o] <= tk.thr[o].key);
+          PSTAT(a, 11, pass);  // block top-K merge
           if (__ballot(pass)) wave_topk(tk, lock, nobj, a.K, key, ok, rank);
         }
         r += len;

@@ -154,6 +154,12 @@ struct FastArgs {
   unsigned int* dbg_flag;
   uint64_t lowtab_n;  // entries of lowtab
 #endif
+#ifdef BOTE_PATHSTATS
+  // Path-statistics builds only (scripts/build_variant.sh pstats -DBOTE_PATHSTATS,
+  // scripts/pathstats.py): per wave-step, how often each rare path of the group
+  // kernel runs for the wavefront (any lane taking it), 64 counters
+  unsigned long long* pstats;
+#endif
 #ifdef BOTE_ABLATION
   // Timing-diagnostics builds only (scripts/build_variant.sh NAME -DBOTE_ABLATION,
   // env BOTE_ABLATE; results are wrong when set).  The product library is
@@ -173,6 +179,18 @@ struct FastArgs {
 #else
 #define GASSERT(a, cond, code) \
   do {                         \
+  } while (0)
+#endif
+#ifdef BOTE_PATHSTATS
+// counter k += 1 when any active lane of the wavefront has `cond` (one lane adds)
+#define PSTAT(a, k, cond)                                                                        \
+  do {                                                                                           \
+    const unsigned long long pm_ = __ballot(cond), pa_ = __ballot(1);                            \
+    if (pm_ && (threadIdx.x & 63) == (unsigned)__builtin_ctzll(pa_)) atomicAdd(&(a).pstats[k], 1ull); \
+  } while (0)
+#else
+#define PSTAT(a, k, cond) \
+  do {                    \
   } while (0)
 #endif
 #ifdef BOTE_ABLATION

@@ -7,7 +7,7 @@
 #
 # Steps (outputs under gpurun_out/$TAG/):
 #   smoke    __graft_entry__.py (smoke on cuda:0)
-#   tests    pytest -m gpu over TEST_FILES (default tests/; PYTEST_K="-k expr" to select)
+#   tests    pytest -m gpu over TEST_FILES (default tests/; PYTEST_EXPR: a -k expression)
 #   bench    bench.py with the CPU baseline, for each workload in WLS
 #   ab       A/B timing of library variants: VARIANTS="default lib_x ..." (lib_x:
 #            fantoch_amd/lib_x/libbote_hip.so, scripts/build_variant.sh), REPS
@@ -18,6 +18,7 @@
 #   pmc      extra PMC passes: PASSES="ctr ...;ctr ..." over bench.py BENCH_ARGS
 #   shards   kernel trace of scripts/shard_ablate.py (per-dispatch cost of shards)
 #   ablate   scripts/ablate.py masks ABL on the -DBOTE_ABLATION library (lib_abl)
+#   pstats   scripts/pathstats.py on the -DBOTE_PATHSTATS library (lib_pstats), for each workload in WLS
 #   oracle   the CPU oracle over R=64 n=7 chunks from ORACLE_BEGIN for
 #            ORACLE_SECONDS (scripts/oracle_full_sweep.py --partial; state to
 #            gpurun_out/$TAG/oracle_chunks.jsonl, merged into the fixture here)
@@ -36,7 +37,9 @@ step_smoke() {
 }
 
 step_tests() {
-  timeout -k 10 1100 python -u -m pytest ${TEST_FILES:-tests/} -m gpu -x -v --timeout 400 --timeout-method thread ${PYTEST_K:-} \
+  local sel=(-m gpu)
+  [ -n "${PYTEST_EXPR:-}" ] && sel=(-m gpu -k "$PYTEST_EXPR")
+  timeout -k 10 1100 python -u -m pytest ${TEST_FILES:-tests/} "${sel[@]}" -x -v --timeout 400 --timeout-method thread \
     > "$O/gpu_tests.log" 2>&1 || fail tests $? "$O/gpu_tests.log"
   echo "tests ok: $(tail -1 "$O/gpu_tests.log")"
 }
@@ -106,6 +109,14 @@ step_ablate() {
   BOTE_LIB_PATH=fantoch_amd/lib_abl/libbote_hip.so timeout -k 10 300 python -u scripts/ablate.py ${ABL:-0} \
     > "$O/ablate.log" 2>&1 || fail ablate $? "$O/ablate.log"
   grep -v amdgpu.ids "$O/ablate.log"
+}
+
+step_pstats() {
+  for wl in $WLS; do
+    BOTE_LIB_PATH=fantoch_amd/lib_pstats/libbote_hip.so timeout -k 10 300 python -u scripts/pathstats.py "$wl" \
+      > "$O/pstats_$wl.json" 2> "$O/pstats_$wl.err" || fail "pstats $wl" $? "$O/pstats_$wl.err"
+    echo "pstats $wl: $(tr -d '\n' < "$O/pstats_$wl.json" | cut -c1-600)"
+  done
 }
 
 step_oracle() {
