@@ -98,11 +98,17 @@ def host_cpu_share() -> int:
     return max(1, n)
 
 
-def cpu_baseline(planet, n, budget_s=10.0):
+def cpu_baseline(planet, n, keys=0, objectives=None, budget_s=10.0, nsample=1_000_000, seed=0x5EED0001,
+                 cap_s=60.0):
     """The reference-faithful CPU restatement (oracle/, 'port') timed on this
-    host over bounded contiguous slices of the same rank space: (i) one thread,
-    the reference's own parallelism for a single client set (search.rs:209-211:
-    rayon only splits client sets), and (ii) all of this job's CPUs."""
+    host over a seeded uniform sample of the workload's rank space (BASELINE.md:
+    "uniform sample of 10^6 ranks (fixed seed)"), with the workload's own key
+    set and objectives (config 5: the extended keys, CONFIG5_OBJECTIVES):
+      * all of this job's CPUs over the 10^6 sampled ranks (fewer only when the
+        estimated time exceeds cap_s; the line then says how many);
+      * one thread -- the reference's own parallelism for a single client set
+        (search.rs:209-211: rayon only splits client sets) -- over a prefix of
+        the same draw sized to about budget_s of work."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import numpy as np
 
@@ -110,31 +116,38 @@ def cpu_baseline(planet, n, budget_s=10.0):
     from fantoch_amd import _lib
     from fantoch_amd.bote import DEFAULT_OBJECTIVES
 
+    objs = list(objectives or DEFAULT_OBJECTIVES)
     o = O.OraclePlanet.of(planet)
     srv = np.arange(planet.R, dtype=np.uint32)
     total = _lib.binomial(planet.R, n)
     rp = (110.0, 35.0, 0.0, 15.0)
-    mid = total // 2
+    ranks = np.random.default_rng(seed).integers(0, total, size=nsample, dtype=np.uint64)
 
-    def timed(threads, budget):
-        cal = 500 * threads  # calibrate, then size the sample to ~budget of wall time
+    def run(count, threads):
         t0 = time.perf_counter()
-        o.sweep(srv, srv, n, mid, mid + cal, DEFAULT_OBJECTIVES, 100, rp, 2, threads)
-        dt = max(time.perf_counter() - t0, 1e-6)
-        count = int(max(cal, min(total - mid, cal * budget / dt)))
-        t0 = time.perf_counter()
-        o.sweep(srv, srv, n, mid, mid + count, DEFAULT_OBJECTIVES, 100, rp, 2, threads)
-        return count, time.perf_counter() - t0
+        o.sweep_ranks(srv, srv, n, ranks[:count], objs, 100, rp, 2, threads, keys)
+        return time.perf_counter() - t0
 
     share = host_cpu_share()
-    c1, d1 = timed(1, budget_s)
-    cn, dn = timed(share, budget_s) if share > 1 else (c1, d1)
+    cal = 200
+    rate1 = cal / max(run(cal, 1), 1e-6)
+    c1 = int(max(cal, min(nsample, rate1 * budget_s)))
+    d1 = run(c1, 1)
+    if share > 1:
+        calc = min(nsample, 200 * share)
+        raten = calc / max(run(calc, share), 1e-6)
+        cn = int(min(nsample, max(calc, raten * cap_s)))
+        dn = run(cn, share)
+    else:
+        cn, dn = c1, d1
+    key_set = "extended key set (Tempo tiny/write + FPaxos all leaders)" if keys else "the 10 compute_stats keys"
     return {"value": cn / dn, "unit": "configs/s", "cores": share, "kind": "port",
-            "sample": f"{cn} consecutive colex ranks from rank {mid} of {total}, full compute_stats + "
-                      f"compute_score + top-K per config (oracle/bote_oracle.cpp, std::thread x {share})",
+            "sample": f"{cn} colex ranks drawn uniformly from [0, {total}) (numpy default_rng({seed:#x})), "
+                      f"{key_set}, {len(objs)} objectives, full compute_stats + compute_score + top-K per config "
+                      f"(oracle/bote_oracle.cpp oracle_sweep_ranks, std::thread x {share})",
             "seconds": round(dn, 3), "nproc": os.cpu_count(), "cpu_share": share,
-            "single_thread": {"value": c1 / d1, "unit": "configs/s", "cores": 1, "sample": f"{c1} ranks from {mid}",
-                              "seconds": round(d1, 3)}}
+            "single_thread": {"value": c1 / d1, "unit": "configs/s", "cores": 1,
+                              "sample": f"the first {c1} ranks of the same draw", "seconds": round(d1, 3)}}
 
 
 GCP_NS = (3, 5, 7, 9, 11, 13)  # Search::compute_configs: n in (min_n..=max_n).step_by(2) (search.rs:241-246)
@@ -418,7 +431,8 @@ def main():
             insts = pmc["valu_insts_per_config"] * shard / 64
             clk = pmc.get("clock_ghz", 2.4)
             valu = {"insts_per_config": pmc["valu_insts_per_config"], "clock_ghz": clk,
-                    "util": insts * 2 / (1024 * kavg_ms * 1e-3 * clk * 1e9), "source": pmc.get("source")}
+                    "util": insts * 2 / (1024 * kavg_ms * 1e-3 * clk * 1e9), "source": pmc.get("source"),
+                    "pmc_build": pmc.get("build")}
         out = {
             "metric": METRIC if args.workload == "r64n7" else f"region configs evaluated/sec, {wl['desc']}",
             "value": total * args.steps / dt,
@@ -443,6 +457,13 @@ def main():
                          "work_def": "W' (DESIGN.md §5, bench.work_per_config_%s)" % ("keys" if wl["keys"] else "group"),
                          "survey_w": W, "survey_w_frac": shard * W / (kavg_ms * 1e-3) / 1e12 / VALU_PEAK_TOPS,
                          "valu_issue": valu, "kernel_ms_avg": kavg_ms,
+                         # the primary utilisation figure: measured VALU issue (SQ_INSTS_VALU x 2 cycles over
+                         # SIMD-cycles); frac above is W' (algorithmic ops) over the lane-op peak and runs
+                         # above issue where W' overcounts the executed instructions (R=128)
+                         "util": valu["util"] if valu else None,
+                         "util_def": "VALU issue: SQ_INSTS_VALU x 2 cycles / (1024 SIMDs x kernel cycles), "
+                                     "profiles/pmc.json",
+                         "frac_vs_util": (achieved / VALU_PEAK_TOPS) / valu["util"] if valu and valu["util"] else None,
                          "kernel": KERNEL_NAMES[sweep.kernel_path()]},
             "world": dict(census, size=world, shard=[b, e]),
             "result_check": {"valid": res.valid, "digest": res.digest, "deferred": sweep.deferred(stream),
@@ -452,10 +473,11 @@ def main():
             out["rehearsal"] = f"{world} ranks on {census['distinct_devices']} GPU(s) over gloo: not a bench line"
         if os.environ.get("BOTE_LIB_PATH"):
             out["config"]["lib_path"] = os.environ["BOTE_LIB_PATH"]  # an A/B build, not the product library
-        if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(planet, n)
+        if not args.no_cpu_baseline:  # (after the timed region; at N > 1 on rank 0 only)
+            out["cpu_baseline"] = cpu_baseline(planet, n, wl["keys"], objectives)
         print(json.dumps(out), flush=True)
     if world > 1:
+        dist.barrier()  # (the other ranks wait for rank 0's CPU baseline)
         dist.destroy_process_group()
 
 

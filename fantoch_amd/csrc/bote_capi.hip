@@ -781,10 +781,10 @@ int bote_sweep_create_keys(const bote_planet* p, const uint32_t* servers, uint32
     std::vector<uint32_t> ident(p->R);
     for (uint32_t i = 0; i < p->R; ++i) ident[i] = i;
     bool cli_ident = nc == p->R && std::equal(clients, clients + nc, ident.begin());
-    uint32_t cq_quads = 0, rq_quads = 0;
-    auto cq = quad_layout(p->lat.data(), p->R, clients, nc, bote::LAT_SHIFT, cq_quads);
+    uint32_t cq_quads = 0, rq_quads = 0, cq_stride = 0, rq_stride = 0;
+    auto cq = quad_layout(p->lat.data(), p->R, clients, nc, bote::LAT_SHIFT, cq_quads, cq_stride);
     std::vector<uint16_t> rq;
-    if (!cli_ident) rq = quad_layout(p->lat.data(), p->R, ident.data(), p->R, bote::LAT_SHIFT, rq_quads);
+    if (!cli_ident) rq = quad_layout(p->lat.data(), p->R, ident.data(), p->R, bote::LAT_SHIFT, rq_quads, rq_stride);
     if (s->cqt.alloc(cq.size() * 2) != hipSuccess || (!cli_ident && s->rqt.alloc(rq.size() * 2) != hipSuccess) ||
         s->queue.alloc(QUEUE_CAP * 8) != hipSuccess || s->qcount.alloc(16) != hipSuccess)
       return cleanup(fail(BOTE_E_NOMEM, "hipMalloc fast-path buffers"));
@@ -797,6 +797,8 @@ int bote_sweep_create_keys(const bote_planet* p, const uint32_t* servers, uint32
     f.R = p->R;
     f.cq_quads = cq_quads;
     f.rq_quads = cli_ident ? cq_quads : rq_quads;
+    f.cq_stride = cq_stride;
+    f.rq_stride = cli_ident ? cq_stride : rq_stride;
     f.srv = s->srv.as<uint32_t>();
     f.ns = ns;
     f.keys = keys;

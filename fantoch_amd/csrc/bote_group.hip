@@ -95,23 +95,29 @@ struct GCfg {
   static_assert(!RX || (F <= 4 && KQ <= 4), "position table holds 4 fixed members");
 };
 
-// per-wave group line: [rx: ns x 16 B (n <= 7)][mF: cq_quads+1 uint2][Upk: FP*KQ u32][fS1: F u32][fV: F f32],
+// per-wave group line: [rx: ns x 16 B (n <= 7)][mF: cq_stride uint2][Upk: FP*KQ u32][fS1: F u32][fV: F f32],
 // padded to 16 bytes
 __host__ __device__ inline uint32_t gline_rx_bytes(const FastArgs& a, int N) { return N <= 7 && a.grx ? a.ns * 16 : 0u; }
 __host__ __device__ inline uint32_t gline_bytes(const FastArgs& a, int N, int KQ) {
   const int F = N - 3, FP = (F + 1) / 2;
-  return (gline_rx_bytes(a, N) + (a.cq_quads + 1) * 8 + (uint32_t)(FP * KQ + 2 * F) * 4 + 15) & ~15u;
+  return (gline_rx_bytes(a, N) + a.cq_stride * 8 + (uint32_t)(FP * KQ + 2 * F) * 4 + 15) & ~15u;
 }
 
-// region 0: PERM kernels: per wave, gslots client lines of (cq_quads + 1)
+// one wave's client lines (gslots lines of cq_stride quads, then the slots'
+// keys), rounded to 16 B: the lines are read 16 B at a time (ds_read_b128)
+__host__ __device__ inline uint32_t lines_wave_bytes(const FastArgs& a) {
+  return (a.gslots * (a.cq_stride * 8 + 4) + 15) & ~15u;
+}
+
+// region 0: PERM kernels: per wave, gslots client lines of cq_stride
 // quads; otherwise the qtab (N * NLW member planes of 1 << gqsh bytes)
 __host__ __device__ inline size_t group_layout(const FastArgs& a, int N, int NLW, int KQ, bool perm, size_t* off) {
   size_t o = 0;
   off[0] = o;
-  o += perm ? (size_t)(a.gbd / 64) * a.gslots * ((a.cq_quads + 1) * 8 + 4) : ((size_t)N * NLW) << a.gqsh;
+  o += perm ? (size_t)(a.gbd / 64) * lines_wave_bytes(a) : ((size_t)N * NLW) << a.gqsh;
   o = (o + 15) & ~(size_t)15;
-  off[1] = o; o += (size_t)a.R * (a.cq_quads + 1) * 8;
-  off[2] = o; o += a.rq_separate ? (size_t)a.R * (a.rq_quads + 1) * 8 : 0;
+  off[1] = o; o += (size_t)a.R * a.cq_stride * 8;
+  off[2] = o; o += a.rq_separate ? (size_t)a.R * a.rq_stride * 8 : 0;
   off[3] = o; o += (size_t)a.ns * 4;  // srv
   o = (o + 7) & ~(size_t)7;
   off[4] = o; o += (size_t)a.ns * 8;  // lrec: (cs1, f32 vcol) per position
@@ -417,12 +423,12 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
 
   // ---- stage: quad matrices, server list, binomials; then per-position sums
   {
-    const uint32_t cw = a.R * (a.cq_quads + 1) * 2;
+    const uint32_t cw = a.R * a.cq_stride * 2;
     const uint32_t* src = (const uint32_t*)a.cqt;
     uint32_t* dst = (uint32_t*)(smem + off[1]);
     for (uint32_t i = tid; i < cw; i += BD) dst[i] = src[i];
     if (a.rq_separate) {
-      const uint32_t rw = a.R * (a.rq_quads + 1) * 2;
+      const uint32_t rw = a.R * a.rq_stride * 2;
       const uint32_t* rs = (const uint32_t*)a.rqt;
       uint32_t* rd = (uint32_t*)(smem + off[2]);
       for (uint32_t i = tid; i < rw; i += BD) rd[i] = rs[i];
@@ -438,8 +444,8 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
   if constexpr (BIN)
     for (uint32_t i = tid; i < (BD >> 6) * N * 64; i += BD) ((uint32_t*)(smem + off[14]))[i] = 0;
   __syncthreads();
-  const uint32_t cstride = (a.cq_quads + 1) * 8;  // bytes per CQT column
-  const uint32_t rstride = (a.rq_quads + 1) * 8;
+  const uint32_t cstride = a.cq_stride * 8;  // bytes per CQT column
+  const uint32_t rstride = a.rq_stride * 8;
   for (uint32_t i = tid; i < a.ns; i += BD) {
     const uint32_t col = cqt + srv[i] * cstride;
     uint64_t c1 = 0, c2 = 0;
@@ -462,7 +468,7 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
   const uint32_t qlane = qtab + tid * 4;
   // PERM: this wave's client lines (one per distinct (p1, p2) of a step),
   // then the pairs' keys (lowtab entries)
-  const uint32_t lines = qtab + wid * a.gslots * (cstride + 4);
+  const uint32_t lines = qtab + wid * lines_wave_bytes(a);
   const uint32_t keys = lines + a.gslots * cstride;
   const uint32_t gl = LB + (uint32_t)off[8] + wid * gline_bytes(a, N, KQ);  // this wave's group line
   const uint32_t rxt = gl;                                                 // per-position table (RX)
@@ -1097,9 +1103,27 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
                   hi = pk_min(pk_min(as_us2(wa.y), as_us2(wb.y) | J1), pk_min(as_us2(wc.y) | J2, as_us2(wf.y)));
                 }
               };
-              auto quad = [&](auto lines_c, uint32_t g8, uint32_t mlo, uint32_t mhi) {
-                us2 lo, hi;
-                nearest(lines_c, g8, lo, hi);
+              // two quads at once (g16: a 16-B aligned offset): one ds_read_b128
+              // per source (4 LDS cycles for 16 B per lane, where the pair of
+              // 8-B reads the compiler would merge into a ds_read2_b64 takes 8;
+              // the column stride is an odd number of 16-B units: quad_stride)
+              auto nearest2 = [&](auto lines_c, uint32_t g16, us2& lo0, us2& hi0, us2& lo1, us2& hi1) {
+                const uint4 wa = l128(c0 + g16);
+                if constexpr (decltype(lines_c)::value) {
+                  const uint4 wl = l128(ll + g16);
+                  lo0 = pk_min(as_us2(wa.x), as_us2(wl.x));
+                  hi0 = pk_min(as_us2(wa.y), as_us2(wl.y));
+                  lo1 = pk_min(as_us2(wa.z), as_us2(wl.z));
+                  hi1 = pk_min(as_us2(wa.w), as_us2(wl.w));
+                } else {
+                  const uint4 wb = l128(c1 + g16), wc = l128(c2 + g16), wf = l128(mfl + g16);
+                  lo0 = pk_min(pk_min(as_us2(wa.x), as_us2(wb.x) | J1), pk_min(as_us2(wc.x) | J2, as_us2(wf.x)));
+                  hi0 = pk_min(pk_min(as_us2(wa.y), as_us2(wb.y) | J1), pk_min(as_us2(wc.y) | J2, as_us2(wf.y)));
+                  lo1 = pk_min(pk_min(as_us2(wa.z), as_us2(wb.z) | J1), pk_min(as_us2(wc.z) | J2, as_us2(wf.z)));
+                  hi1 = pk_min(pk_min(as_us2(wa.w), as_us2(wb.w) | J1), pk_min(as_us2(wc.w) | J2, as_us2(wf.w)));
+                }
+              };
+              auto quad_at = [&](us2 lo, us2 hi, uint32_t mlo, uint32_t mhi) {
                 const uint32_t L = as_u32(lo), H = as_u32(hi);
 #ifdef BOTE_DEBUG
                 // every client's nearest-member tag names a member (low 4 bits)
@@ -1148,6 +1172,17 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
                   }
                 }
               };
+              auto quad = [&](auto lines_c, uint32_t g8, uint32_t mlo, uint32_t mhi) {
+                us2 lo, hi;
+                nearest(lines_c, g8, lo, hi);
+                quad_at(lo, hi, mlo, mhi);
+              };
+              auto quad2 = [&](auto lines_c, uint32_t g16) {
+                us2 lo0, hi0, lo1, hi1;
+                nearest2(lines_c, g16, lo0, hi0, lo1, hi1);
+                quad_at(lo0, hi0, ~0u, ~0u);
+                quad_at(lo1, hi1, ~0u, ~0u);
+              };
               auto flush = [&]() {
 #pragma unroll
                 for (int t = 0; t < NT; ++t) {
@@ -1163,13 +1198,14 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
               // (XK: 2 quads per iteration; its 4 tables' temporaries of 4
               // unrolled quads spill)
               constexpr uint32_t U = XK ? 2u : (uint32_t)BOTE_GROUP_UNROLL;
+              static_assert(U % 2 == 0, "quads are read in 16-B pairs");
               auto clients = [&](auto lines_c) {
                 const uint32_t fU = a.g_flush / U ? a.g_flush / U : 1u;
                 uint32_t g = 0, k = 0;
                 if (a.g_flush >= U) {
                   for (; g + U <= nql; g += U) {
 #pragma unroll
-                    for (uint32_t u = 0; u < U; ++u) quad(lines_c, g * 8 + 8 * u, ~0u, ~0u);
+                    for (uint32_t u = 0; u < U; u += 2) quad2(lines_c, g * 8 + 8 * u);  // (g, U even: 16-B aligned)
                     if (++k == fU) {
                       flush();
                       k = 0;
@@ -1250,7 +1286,14 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
                     for (; g + UB <= nql; g += UB) {
                       uint32_t Lk[UB], Hk[UB];
 #pragma unroll
-                      for (uint32_t u = 0; u < UB; ++u) quad_keys(lines_c, g * 8 + 8 * u, Lk[u], Hk[u]);
+                      for (uint32_t u = 0; u < UB; u += 2) {  // (g, UB even: 16-B aligned pairs of quads)
+                        us2 lo0, hi0, lo1, hi1;
+                        nearest2(lines_c, g * 8 + 8 * u, lo0, hi0, lo1, hi1);
+                        Lk[u] = as_u32(lo0);
+                        Hk[u] = as_u32(hi0);
+                        Lk[u + 1] = as_u32(lo1);
+                        Hk[u + 1] = as_u32(hi1);
+                      }
 #pragma unroll
                       for (uint32_t u = 0; u < UB; ++u) quad_bin(Lk[u], Hk[u], 4u);
                       if (++k == fU) {

@@ -196,13 +196,21 @@ bool pick_group_geometry(uint32_t bd, int occ, uint32_t gslots, uint32_t best_bd
   return bd < best_bd;
 }
 
+uint32_t quad_stride(uint32_t quads) {
+  uint32_t s = quads + 1;
+  if (s & 1) ++s;
+  if ((s / 2) % 2 == 0) s += 2;
+  return s;
+}
+
 std::vector<uint16_t> quad_layout(const uint16_t* lat, uint32_t R, const uint32_t* rows, uint32_t nrows,
-                                  uint32_t shift, uint32_t& quads) {
+                                  uint32_t shift, uint32_t& quads, uint32_t& stride) {
   quads = (nrows + 3) / 4;
-  const uint32_t stride = (quads + 1) * 4;  // u16 per column (one pad quad)
-  std::vector<uint16_t> m((size_t)R * stride, 0);
+  stride = quad_stride(quads);
+  const uint32_t su16 = stride * 4;  // u16 per column
+  std::vector<uint16_t> m((size_t)R * su16, 0);
   for (uint32_t t = 0; t < R; ++t)
-    for (uint32_t c = 0; c < nrows; ++c) m[(size_t)t * stride + c] = (uint16_t)(lat[(size_t)rows[c] * R + t] << shift);
+    for (uint32_t c = 0; c < nrows; ++c) m[(size_t)t * su16 + c] = (uint16_t)(lat[(size_t)rows[c] * R + t] << shift);
   return m;
 }
 

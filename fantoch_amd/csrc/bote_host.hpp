@@ -66,9 +66,14 @@ bool pick_group_geometry(uint32_t bd, int occ, uint32_t gslots, uint32_t best_bd
 // ------------------------------------------------------------ layouts ----
 // Column-major packed-u16 quad layout of `rows` (client ids) against every
 // region t of an R x R matrix (row = from): entry [t][c] = lat[rows[c]][t] <<
-// shift, column stride (quads + 1) * 4 u16 (one pad quad).
+// shift, column stride `stride` quads (quad_stride: at least one pad quad).
 std::vector<uint16_t> quad_layout(const uint16_t* lat, uint32_t R, const uint32_t* rows, uint32_t nrows,
-                                  uint32_t shift, uint32_t& quads);
+                                  uint32_t shift, uint32_t& quads, uint32_t& stride);
+// Column stride in quads (8 B) for `quads` data quads: at least quads + 1,
+// and an odd number of 16-B units, so that a column starts 16-B aligned
+// (ds_read_b128 of two quads) and 16 lanes at consecutive columns hit 16
+// distinct 4-bank groups (conflict-free 16-B reads, MI355X_MICROARCH.md LDS).
+uint32_t quad_stride(uint32_t quads);
 // Packed (p0 | p1 << 8 | p2 << 16) 3-subsets of [0, m) in colex order.
 std::vector<uint32_t> low_table(uint32_t m);
 // The fast path's preconditions (bote_sweep.hip header): every latency <=

@@ -82,10 +82,11 @@ struct SingleArgs {
 // ---- fast-path sweep (bote_sweep.hip)
 constexpr uint32_t FAST_BD = 256;
 struct FastArgs {
-  const uint2* cqt;  // client quads, column-major, column stride (cq_quads + 1) uint2
+  const uint2* cqt;  // client quads, column-major, column stride cq_stride uint2 (quad_stride)
   const uint2* rqt;  // region quads (rows = all regions), used when rq_separate
   int rq_separate;
   uint32_t R, cq_quads, rq_quads;
+  uint32_t cq_stride, rq_stride;  // quads per column (>= quads + 1; an odd number of 16-B units)
   const uint32_t* srv;
   uint32_t ns;
   int srv_identity;  // srv[p] == p

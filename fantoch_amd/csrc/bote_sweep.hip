@@ -49,8 +49,8 @@ struct FastSmem {
 __host__ __device__ inline size_t fast_layout(const FastArgs& a, int N, int NLW, size_t* off) {
   size_t o = 0;
   off[0] = o; o += (size_t)N * FAST_BD * NLW * 4;  // qtab first: offsets stay small
-  off[1] = o; o += (size_t)a.R * (a.cq_quads + 1) * 8;
-  off[2] = o; o += a.rq_separate ? (size_t)a.R * (a.rq_quads + 1) * 8 : 0;
+  off[1] = o; o += (size_t)a.R * a.cq_stride * 8;
+  off[2] = o; o += a.rq_separate ? (size_t)a.R * a.rq_stride * 8 : 0;
   off[3] = o; o += (size_t)a.ns * 4;  // srv
   off[4] = o; o += (size_t)a.ns * 4;  // cs1
   o = (o + 15) & ~(size_t)15;
@@ -261,12 +261,12 @@ __global__ void __launch_bounds__(FAST_BD, 4) sweep_fast_kernel(FastArgs a) {
 
   // ---- stage: quad matrices, server list, binomials; then per-position sums
   {
-    const uint32_t cw = a.R * (a.cq_quads + 1) * 2;  // 32-bit words
+    const uint32_t cw = a.R * a.cq_stride * 2;  // 32-bit words
     const uint32_t* src = (const uint32_t*)a.cqt;
     uint32_t* dst = (uint32_t*)(smem + s.cqt);
     for (uint32_t i = tid; i < cw; i += FAST_BD) dst[i] = src[i];
     if (a.rq_separate) {
-      const uint32_t rw = a.R * (a.rq_quads + 1) * 2;
+      const uint32_t rw = a.R * a.rq_stride * 2;
       const uint32_t* rs = (const uint32_t*)a.rqt;
       uint32_t* rd = (uint32_t*)(smem + s.rqt);
       for (uint32_t i = tid; i < rw; i += FAST_BD) rd[i] = rs[i];
@@ -276,8 +276,8 @@ __global__ void __launch_bounds__(FAST_BD, 4) sweep_fast_kernel(FastArgs a) {
   for (uint32_t i = tid; i < (a.ns + 1) * (N + 1); i += FAST_BD) s.binom[i] = a.binom[i];
   topk_init(s.tk, a.n_obj);
   __syncthreads();
-  const uint32_t cstride = (a.cq_quads + 1) * 8;  // bytes per CQT column
-  const uint32_t rstride = (a.rq_quads + 1) * 8;
+  const uint32_t cstride = a.cq_stride * 8;  // bytes per CQT column
+  const uint32_t rstride = a.rq_stride * 8;
   for (uint32_t i = tid; i < a.ns; i += FAST_BD) {
     const uint32_t col = s.cqt + s.srv[i] * cstride;
     uint64_t c1 = 0, c2 = 0;

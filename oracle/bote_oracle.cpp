@@ -892,6 +892,77 @@ int oracle_sweep_x(void* h, const uint32_t* servers, uint32_t ns, const uint32_t
   ORACLE_CATCH
 }
 
+// oracle_sweep_x over an explicit list of colex ranks (any order, repeats
+// counted again): the CPU baseline's seeded uniform sample (bench.py).  Same
+// per-config work: unrank, compute_stats[_x], compute_score, digest, the
+// objectives' top-K.
+int oracle_sweep_ranks(void* h, const uint32_t* servers, uint32_t ns, const uint32_t* clients, uint32_t nc,
+                       uint32_t n, const uint64_t* ranks, uint64_t nranks, const uint32_t* objs, uint32_t n_obj,
+                       uint32_t K, const double* rparams, int ft_metric, uint32_t keys, uint32_t threads,
+                       uint64_t* out_key, uint64_t* out_rank, uint32_t* out_cnt, uint64_t* out_valid,
+                       uint64_t* out_digest) {
+  ORACLE_TRY
+  const Planet* P = (Planet*)h;
+  Bote b{P};
+  std::vector<uint32_t> cl(clients, clients + nc);
+  std::vector<Objective> ob(n_obj);
+  for (uint32_t o = 0; o < n_obj; ++o) ob[o] = {objs[2 * o], objs[2 * o + 1]};
+  RankingParams rp{rparams[0], rparams[1], rparams[2], rparams[3], 3, 13, ft_metric};
+  Binom B(ns, n);
+  const uint64_t total = B(ns, n);
+  for (uint64_t i = 0; i < nranks; ++i)
+    if (ranks[i] >= total) throw Panic("rank out of range");
+  if (threads == 0) threads = 1;
+  std::vector<std::vector<TopK>> tops(threads, std::vector<TopK>(n_obj, TopK{K, {}}));
+  std::vector<uint64_t> valid(threads, 0), digest(threads, 0);
+  std::vector<std::string> errs(threads);
+  auto work = [&](uint32_t t) {
+    try {
+      std::vector<uint32_t> pos(n), cfg(n);
+      for (uint64_t i = nranks * t / threads; i < nranks * (t + 1) / threads; ++i) {
+        const uint64_t r = ranks[i];
+        colex_unrank(B, r, n, ns, pos.data());
+        for (uint32_t j = 0; j < n; ++j) cfg[j] = servers[pos[j]];
+        ProtocolStats st;
+        if (keys) compute_stats_x(b, cfg, cl, st);
+        else compute_stats(b, cfg, cl, st);
+        double score;
+        if (compute_score(n, st, rp, score)) valid[t]++;
+        digest[t] += config_digest(r, st);
+        for (uint32_t o = 0; o < n_obj; ++o) {
+          uint64_t key;
+          if (objective_key(ob[o], n, st, rp, key)) tops[t][o].push(key, r);
+        }
+      }
+    } catch (const std::exception& ex) {
+      errs[t] = ex.what();
+    }
+  };
+  std::vector<std::thread> pool;
+  for (uint32_t t = 1; t < threads; ++t) pool.emplace_back(work, t);
+  work(0);
+  for (auto& th : pool) th.join();
+  for (auto& e : errs)
+    if (!e.empty()) throw Panic(e);
+  *out_valid = 0;
+  *out_digest = 0;
+  for (uint32_t t = 0; t < threads; ++t) {
+    *out_valid += valid[t];
+    *out_digest += digest[t];
+  }
+  for (uint32_t o = 0; o < n_obj; ++o) {
+    TopK m{K, {}};
+    for (uint32_t t = 0; t < threads; ++t)
+      for (auto& e : tops[t][o].v) m.push(e.first, e.second);
+    out_cnt[o] = (uint32_t)m.v.size();
+    for (size_t i = 0; i < m.v.size(); ++i) {
+      out_key[(size_t)o * K + i] = m.v[i].first;
+      out_rank[(size_t)o * K + i] = m.v[i].second;
+    }
+  }
+  ORACLE_CATCH
+}
+
 int oracle_sweep(void* h, const uint32_t* servers, uint32_t ns, const uint32_t* clients,
                  uint32_t nc, uint32_t n, uint64_t rb, uint64_t re, const uint32_t* objs,
                  uint32_t n_obj, uint32_t K, const double* rparams, int ft_metric,

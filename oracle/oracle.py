@@ -73,6 +73,9 @@ def lib():
         L.oracle_sweep_x.argtypes = [C.c_void_p, u32p, C.c_uint32, u32p, C.c_uint32, C.c_uint32, C.c_uint64,
                                      C.c_uint64, u32p, C.c_uint32, C.c_uint32, f64p, C.c_int, C.c_uint32,
                                      C.c_uint32, u64p, u64p, u32p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
+        L.oracle_sweep_ranks.argtypes = [C.c_void_p, u32p, C.c_uint32, u32p, C.c_uint32, C.c_uint32, u64p,
+                                         C.c_uint64, u32p, C.c_uint32, C.c_uint32, f64p, C.c_int, C.c_uint32,
+                                         C.c_uint32, u64p, u64p, u32p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
         L.oracle_moments_x.argtypes = [C.c_void_p, u32p, C.c_uint32, C.c_uint32, u32p, C.c_uint32, C.c_uint32,
                                        u64p, u64p, u64p, u64p, u32p]
         L.oracle_sweep.argtypes = [C.c_void_p, u32p, C.c_uint32, u32p, C.c_uint32, C.c_uint32,
@@ -210,6 +213,25 @@ class OraclePlanet:
                                     ft_metric, keys, threads, kv, ranks, cnt, C.byref(valid),
                                     C.byref(digest)))
         tops = [list(zip(kv[o * K:o * K + cnt[o]].tolist(), ranks[o * K:o * K + cnt[o]].tolist()))
+                for o in range(nobj)]
+        return tops, valid.value, digest.value
+
+    def sweep_ranks(self, servers, clients, n: int, ranks, objectives, K: int,
+                    rparams=(110.0, 35.0, 0.0, 15.0), ft_metric: int = 2, threads: int = 1, keys: int = 0):
+        """sweep over an explicit list of colex ranks (the CPU baseline's seeded
+        uniform sample): the same per-config work as sweep()."""
+        s, c = _u32(servers), _u32(clients)
+        rk = np.ascontiguousarray(np.asarray(ranks, dtype=np.uint64))
+        objs = _u32(np.asarray(objectives, dtype=np.uint32).reshape(-1))
+        nobj = len(objs) // 2
+        kv = np.zeros(nobj * K, np.uint64)
+        out_r = np.zeros(nobj * K, np.uint64)
+        cnt = np.zeros(nobj, np.uint32)
+        valid, digest = C.c_uint64(), C.c_uint64()
+        rp = np.asarray(rparams, dtype=np.float64)
+        _check(lib().oracle_sweep_ranks(self.h, s, len(s), c, len(c), n, rk, len(rk), objs, nobj, K, rp, ft_metric,
+                                        keys, threads, kv, out_r, cnt, C.byref(valid), C.byref(digest)))
+        tops = [list(zip(kv[o * K:o * K + cnt[o]].tolist(), out_r[o * K:o * K + cnt[o]].tolist()))
                 for o in range(nobj)]
         return tops, valid.value, digest.value
 

@@ -161,13 +161,19 @@ static void check_layouts() {
   for (uint32_t i = 0; i < R; ++i)
     for (uint32_t j = 0; j < R; ++j) lat[i * R + j] = i == j ? 0 : (uint16_t)(10 + 3 * i + j);
   const uint32_t rows[] = {4, 1, 7, 0, 8};
-  uint32_t quads = 0;
-  const auto m = quad_layout(lat.data(), R, rows, 5, 4, quads);
+  uint32_t quads = 0, stride = 0;
+  const auto m = quad_layout(lat.data(), R, rows, 5, 4, quads, stride);
   CHECK(quads == 2);
-  CHECK(m.size() == (size_t)R * (quads + 1) * 4);
+  CHECK(stride == 6);  // >= quads + 1, an odd number of 16-B units
+  CHECK(m.size() == (size_t)R * stride * 4);
   for (uint32_t t = 0; t < R; ++t)
-    for (uint32_t c = 0; c < (quads + 1) * 4; ++c)
-      CHECK(m[t * (quads + 1) * 4 + c] == (c < 5 ? (uint16_t)(lat[rows[c] * R + t] << 4) : 0));
+    for (uint32_t c = 0; c < stride * 4; ++c)
+      CHECK(m[t * stride * 4 + c] == (c < 5 ? (uint16_t)(lat[rows[c] * R + t] << 4) : 0));
+  for (uint32_t q = 0; q < 300; ++q) {
+    const uint32_t s = quad_stride(q);
+    CHECK(s >= q + 1 && s % 2 == 0 && (s / 2) % 2 == 1 && s <= q + 4);
+  }
+  CHECK(quad_stride(16) == 18 && quad_stride(32) == 34);
   const auto lt = low_table(10);
   CHECK(lt.size() == binom_u64(10, 3));
   for (size_t i = 0; i < lt.size(); ++i) {

@@ -125,3 +125,20 @@ def test_sweep_digest_is_the_written_definition(planet, n, keys):
                     words += [(w, int(a1[i, f, l]) & 0xFFFFFFFF), (w + 1, (q ^ (q >> 32)) & 0xFFFFFFFF)]
         want += _digest(r, int(lead[i]), words)
     assert dig == want % (1 << 64)
+
+
+@pytest.mark.parametrize("keys", [0, 1])
+def test_sweep_ranks_equals_sweep_on_a_range(keys):
+    """oracle_sweep_ranks (the CPU baseline's seeded uniform sample) does the
+    streaming sweep's per-config work: over an explicit list of a range's
+    ranks, shuffled, it returns the range sweep's valid count, digest and top-K."""
+    p = Planet.new()
+    o = O.OraclePlanet.of(p)
+    s = np.arange(p.R, dtype=np.uint32)
+    objs = [(0, 0), (1, 0), (1, 1), (2, 0), (1, 4)] + ([(1, 10), (1, 13), (1, 18)] if keys else [])
+    want = o.sweep(s, s, 5, 1000, 3000, objs, 16, threads=2, keys=keys)
+    ranks = np.random.default_rng(7).permutation(np.arange(1000, 3000, dtype=np.uint64))
+    got = o.sweep_ranks(s, s, 5, ranks, objs, 16, threads=3, keys=keys)
+    assert got == want
+    with pytest.raises(Exception):
+        o.sweep_ranks(s, s, 5, np.array([15504], np.uint64), objs, 16)  # C(20, 5): out of range
