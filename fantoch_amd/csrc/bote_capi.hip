@@ -903,9 +903,11 @@ int bote_sweep_create_keys(const bote_planet* p, const uint32_t* servers, uint32
       // hold (a step has 7.7 distinct (p1, p2) on average at R=64 n=7, 4.0 at
       // R=128 n=6).  pick_group_geometry keeps the best.
       // the member-binned client loop on the base key set: bench-shaped
-      // sweeps (server identity, digest, F1F2: the SI kernels) with >= 96
-      // clients, where the bin fields cannot overflow
-      f.gbins = !keys && s->def_obj && bote::group_uses_lines(n) && nc >= 96 && nc < 256 && f.srv_identity &&
+      // sweeps (server identity, digest, F1F2: the SI kernels) with >= 32
+      // clients, where the bin fields cannot overflow (R=64 n=7: 14.26 vs
+      // 14.89 ms for the register lookups, profiles/r04c; R=128 n=6: 168 vs
+      // 180 ms, round 3)
+      f.gbins = !keys && s->def_obj && bote::group_uses_lines(n) && nc >= 32 && nc < 256 && f.srv_identity &&
                 f.want_digest && f.ft_metric == 2 && (uint64_t)nc * (16ull * maxlat + 15) < (1ull << 24) &&
                 (uint64_t)nc * maxlat < (1ull << 16) &&  // (packed member-pair bins)
                 2 * (16ull * maxlat + 15) * (16ull * maxlat + 15) < (1ull << 32);

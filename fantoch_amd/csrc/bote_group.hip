@@ -53,6 +53,12 @@ constexpr int GROUP_MAX_BD = 1024;
 #define BOTE_GROUP_WAVES_PERM 4
 #endif
 // qtab member planes are 1 << a.gqsh bytes apart (>= gbd * 4, a power of two)
+// BOTE_GROUP_U8 (a build knob, A/B timing): the PERM client loop on one-byte
+// tables (each table relative to its least member latency; a wavefront whose
+// every config spans < 256 takes it, the others the two-byte planes)
+#ifndef BOTE_GROUP_U8
+#define BOTE_GROUP_U8 0
+#endif
 // BOTE_GROUP_BIN_ALL (a build knob, A/B timing): the member-binned client loop
 // of the extended key set on every PERM kernel
 #ifndef BOTE_GROUP_BIN_ALL
@@ -910,6 +916,31 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
           //      QL, high byte in byte m of QH; members 0..3 in .x, 4..6 in
           //      .y) and the colocated sums over the members
           uint2 QL[NT], QH[NT];
+          // U8: one-byte planes of (Q - base) per table, valid when every
+          // member lies within 255 of the table's least (u8ok)
+          constexpr bool U8 = PERM && !BIN && S32 && BOTE_GROUP_U8;
+          uint2 QB[U8 ? NT : 1];
+          uint32_t qbase[U8 ? NT : 1];
+          bool u8ok = true;
+          if constexpr (U8) {
+#pragma unroll
+            for (int t = 0; t < NT; ++t) {
+              const uint32_t w01 = wp[t][0], w2 = wp[t][1], w34 = wp[t][2];
+              const uint32_t w56 = FP >= 2 ? wp[t][FP >= 2 ? 3 : 2] : w34;  // (N < 7: w34 again)
+              const bool hi56 = N >= 7;  // member 6 present (w56's high half)
+              const us2 mn = pk_min(pk_min(as_us2(w01), as_us2(w34)), as_us2(hi56 ? w56 : (w56 | 0xFFFF0000u)));
+              const us2 mx = pk_max(pk_max(as_us2(w01), as_us2(w34)), as_us2(hi56 ? w56 : (w56 & 0xFFFFu)));
+              const uint32_t base = min(min((uint32_t)mn.x, (uint32_t)mn.y), w2 & 0xFFFFu);
+              const uint32_t top = max(max((uint32_t)mx.x, (uint32_t)mx.y), w2 & 0xFFFFu);
+              u8ok = u8ok && top - base < 256u;
+              const uint32_t bb = base | (base << 16);
+              const uint32_t b01 = w01 - bb, b2 = w2 - base, b34 = w34 - bb;
+              const uint32_t b56 = hi56 ? w56 - bb : w56 - base;
+              QB[t].x = __builtin_amdgcn_perm(b2, b01, 0x0C040200u) | (b34 << 24);
+              QB[t].y = __builtin_amdgcn_perm(b56, b34, 0x0C060402u);
+              qbase[t] = base;
+            }
+          }
           if constexpr (PERM) {
 #pragma unroll
             for (int t = 0; t < NT; ++t) {
@@ -1123,7 +1154,7 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
                   hi1 = pk_min(pk_min(as_us2(wa.w), as_us2(wb.w) | J1), pk_min(as_us2(wc.w) | J2, as_us2(wf.w)));
                 }
               };
-              auto quad_at = [&](us2 lo, us2 hi, uint32_t mlo, uint32_t mhi) {
+              auto quad_at = [&](auto u8_c, us2 lo, us2 hi, uint32_t mlo, uint32_t mhi) {
                 const uint32_t L = as_u32(lo), H = as_u32(hi);
 #ifdef BOTE_DEBUG
                 // every client's nearest-member tag names a member (low 4 bits)
@@ -1139,7 +1170,15 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
                   s2[t] = __builtin_amdgcn_udot2(as_us2(a01), as_us2(a01), s2[t], false);
                   s2[t] = __builtin_amdgcn_udot2(as_us2(a23), as_us2(a23), s2[t], false);
                 };
-                if constexpr (PERM) {
+                if constexpr (U8 && decltype(u8_c)::value) {
+                  // one-byte planes: the selectors (tag, zero, tag, zero) give
+                  // the two clients' table bytes as a u16 pair in one v_perm
+                  const uint32_t s01 = (L & 0x000F000Fu) | 0x0C000C00u, s23 = (H & 0x000F000Fu) | 0x0C000C00u;
+#pragma unroll
+                  for (int t = 0; t < NT; ++t)
+                    acc1(t, as_us2(__builtin_amdgcn_perm(QB[t].y, QB[t].x, s01)),
+                         as_us2(__builtin_amdgcn_perm(QB[t].y, QB[t].x, s23)));
+                } else if constexpr (PERM) {
                   // the 4 clients' member tags as byte selectors, then per
                   // table the low and high bytes of their members' latencies
                   // (v_perm over the byte planes), interleaved into u16 pairs
@@ -1172,16 +1211,16 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
                   }
                 }
               };
-              auto quad = [&](auto lines_c, uint32_t g8, uint32_t mlo, uint32_t mhi) {
+              auto quad = [&](auto lines_c, auto u8_c, uint32_t g8, uint32_t mlo, uint32_t mhi) {
                 us2 lo, hi;
                 nearest(lines_c, g8, lo, hi);
-                quad_at(lo, hi, mlo, mhi);
+                quad_at(u8_c, lo, hi, mlo, mhi);
               };
-              auto quad2 = [&](auto lines_c, uint32_t g16) {
+              auto quad2 = [&](auto lines_c, auto u8_c, uint32_t g16) {
                 us2 lo0, hi0, lo1, hi1;
                 nearest2(lines_c, g16, lo0, hi0, lo1, hi1);
-                quad_at(lo0, hi0, ~0u, ~0u);
-                quad_at(lo1, hi1, ~0u, ~0u);
+                quad_at(u8_c, lo0, hi0, ~0u, ~0u);
+                quad_at(u8_c, lo1, hi1, ~0u, ~0u);
               };
               auto flush = [&]() {
 #pragma unroll
@@ -1199,13 +1238,13 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
               // unrolled quads spill)
               constexpr uint32_t U = XK ? 2u : (uint32_t)BOTE_GROUP_UNROLL;
               static_assert(U % 2 == 0, "quads are read in 16-B pairs");
-              auto clients = [&](auto lines_c) {
+              auto clients = [&](auto lines_c, auto u8_c) {
                 const uint32_t fU = a.g_flush / U ? a.g_flush / U : 1u;
                 uint32_t g = 0, k = 0;
                 if (a.g_flush >= U) {
                   for (; g + U <= nql; g += U) {
 #pragma unroll
-                    for (uint32_t u = 0; u < U; u += 2) quad2(lines_c, g * 8 + 8 * u);  // (g, U even: 16-B aligned)
+                    for (uint32_t u = 0; u < U; u += 2) quad2(lines_c, u8_c, g * 8 + 8 * u);  // (g, U even: 16-B aligned)
                     if (++k == fU) {
                       flush();
                       k = 0;
@@ -1215,11 +1254,11 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
                 }
                 for (uint32_t g0 = g; g0 < nql; g0 += a.g_flush) {
                   const uint32_t ge = min(nql, g0 + a.g_flush);
-                  for (g = g0; g < ge; ++g) quad(lines_c, g * 8, ~0u, ~0u);
+                  for (g = g0; g < ge; ++g) quad(lines_c, u8_c, g * 8, ~0u, ~0u);
                   flush();
                 }
                 if (rem && !ABLATE(a, 1)) {
-                  quad(lines_c, nq * 8, rem >= 2 ? ~0u : 0x0000FFFFu, rem == 3 ? 0x0000FFFFu : 0u);
+                  quad(lines_c, u8_c, nq * 8, rem >= 2 ? ~0u : 0x0000FFFFu, rem == 3 ? 0x0000FFFFu : 0u);
                   flush();
                 }
               };
@@ -1380,8 +1419,24 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
                   if constexpr (S32) S2[t] = (uint32_t)S2[t];  // (< 2^32: FastArgs::s32)
                 }
               } else {
-                if (PERM && use_lines) clients(BoolC<PERM>{});
-                else clients(BoolC<false>{});
+                // U8: the one-byte loop when every config of the wavefront fits
+                // (a uniform branch), then each table's sums shifted by its base:
+                // S1 = S1' + nc b, S2 = S2' + 2 b S1' + nc b^2
+                if (U8 && __ballot(!u8ok) == 0) {
+                  if (use_lines) clients(BoolC<PERM>{}, BoolC<true>{});
+                  else clients(BoolC<false>{}, BoolC<true>{});
+                  if constexpr (U8) {
+#pragma unroll
+                    for (int t = 0; t < NT; ++t) {
+                      const uint32_t b = qbase[t], s1l = S1[t];
+                      S1[t] = s1l + __umul24(nc, b);
+                      S2[t] = (uint32_t)S2[t] + 2u * b * s1l + __umul24(nc, b) * b;  // (S32: < 2^32)
+                    }
+                  }
+                } else {
+                  if (PERM && use_lines) clients(BoolC<PERM>{}, BoolC<false>{});
+                  else clients(BoolC<false>{}, BoolC<false>{});
+                }
               }
               if (ABLATE(a, 1)) {  // timing only: non-degenerate dummy sums
 #pragma unroll
@@ -1729,6 +1784,8 @@ static const void* group_fn(const FastArgs& a, uint32_t n, bool def) {
 #define FN_CASE0(NN) case NN: return a.keys ? nullptr : group_fn_n<NN, false>(a, def);
 #ifdef BOTE_ISA_N7
     FN_CASE(7)
+#elif defined(BOTE_ISA_N6)
+    FN_CASE(6)
 #else
     FN_CASE(4) FN_CASE(5) FN_CASE(6) FN_CASE(7) FN_CASE0(8) FN_CASE0(9) FN_CASE0(10) FN_CASE0(11) FN_CASE0(12)
     FN_CASE0(13) FN_CASE0(14) FN_CASE0(15) FN_CASE0(16)
@@ -1756,6 +1813,8 @@ hipError_t launch_group(const FastArgs& a, uint32_t n, bool def, uint32_t grid, 
   case NN: return a.keys ? hipErrorInvalidValue : launch_group_x<NN, false>(a, def, grid, shm, st);
 #ifdef BOTE_ISA_N7  // (analysis builds only: the n = 7 kernels, for assembly listings)
     GS_CASE(7)
+#elif defined(BOTE_ISA_N6)  // (the n = 6 kernels: BASELINE config 5)
+    GS_CASE(6)
 #else
     GS_CASE(4) GS_CASE(5) GS_CASE(6) GS_CASE(7) GS_CASE0(8) GS_CASE0(9) GS_CASE0(10) GS_CASE0(11) GS_CASE0(12)
     GS_CASE0(13) GS_CASE0(14) GS_CASE0(15) GS_CASE0(16)
