@@ -276,6 +276,12 @@ int bote_colex_unrank(uint64_t rank, uint32_t n, uint32_t ns, uint32_t* out) {
 }
 
 // --------------------------------------------------- single configuration
+// least client count for the member-binned loop on the base key set (a build
+// knob for A/B timing builds only; scripts/build_variant.sh)
+#ifndef BOTE_GBINS_MIN_NC
+#define BOTE_GBINS_MIN_NC 32
+#endif
+
 static int run_single(const bote_planet* p, const uint32_t* servers, uint32_t ns, const uint32_t* clients, uint32_t nc,
                       const uint32_t* froms, uint32_t nf, uint32_t q, uint32_t leader, int mode, uint64_t* out,
                       size_t nout) {
@@ -907,7 +913,7 @@ int bote_sweep_create_keys(const bote_planet* p, const uint32_t* servers, uint32
       // clients, where the bin fields cannot overflow (R=64 n=7: 14.26 vs
       // 14.89 ms for the register lookups, profiles/r04c; R=128 n=6: 168 vs
       // 180 ms, round 3)
-      f.gbins = !keys && s->def_obj && bote::group_uses_lines(n) && nc >= 32 && nc < 256 && f.srv_identity &&
+      f.gbins = !keys && s->def_obj && bote::group_uses_lines(n) && nc >= BOTE_GBINS_MIN_NC && nc < 256 && f.srv_identity &&
                 f.want_digest && f.ft_metric == 2 && (uint64_t)nc * (16ull * maxlat + 15) < (1ull << 24) &&
                 (uint64_t)nc * maxlat < (1ull << 16) &&  // (packed member-pair bins)
                 2 * (16ull * maxlat + 15) * (16ull * maxlat + 15) < (1ull << 32);

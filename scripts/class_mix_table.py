@@ -4,6 +4,9 @@ per 64-config step, reconciled against the measured SQ_INSTS_VALU.
   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -DBOTE_ISA_N7 -g \
       --offload-device-only -S -o kg.s fantoch_amd/csrc/bote_group.hip
   python scripts/class_mix_table.py kg.s ILi7ELb1ELb1ELb1ELb0ELb0E profiles/pmc.json r64n7_n1 > profiles/<tag>_class_mix.md
+  (optional 5th-7th arguments: R n trips -- the workload, and the client
+  loop's unrolled-body trips per step: nq / U; default 64 7 4; the config-5
+  kernel, -DBOTE_ISA_N6: ... r128n6_n1 128 6 8)
 
 Static: instructions per section (scripts/isa_lines.py markers).  Modelled
 dynamic count per step: every basic block of a per-step section runs once per
@@ -13,7 +16,7 @@ step, except
     queue; the block top-K merge under the LDS lock; the sample launch's
     per-chunk minima): 0;
   * the client loop's unrolled body (the lines variant, the block with the
-    most v_dot2 and the fewest LDS reads): nq / U = 16 / 4 = 4 times, the
+    most v_dot2 or LDS adds and the fewest LDS reads): nq / U times, the
     blocks laid out after it (flush, exit) once; the other client-loop bodies
     (no-lines variant, remainder loops): 0;
   * the block top-K merge (wave_topk, inlined; found by its own source
@@ -37,9 +40,11 @@ FAST_RATE, SLOW_RATE = 1.6, 0.95
 
 
 def main():
+    from math import comb
     path, name = sys.argv[1], sys.argv[2]
     pmc = json.load(open(sys.argv[3])).get(sys.argv[4]) if len(sys.argv) > 4 else None
-    groups, steps = 521855, 621216192 / 64.0  # R=64 n=7: C(ns - 1, n - 3) groups, ranks / 64
+    R, n, trips = (int(x) for x in sys.argv[5:8]) if len(sys.argv) > 7 else (64, 7, 4)
+    groups, steps = comb(R - 3, n - 3), comb(R, n) / 64.0  # groups: the fixed parts above position 3
     per_step_groups = groups / steps
     rows = parse(path, name, raw=True)
     secs = DEFAULT_SECTIONS
@@ -71,8 +76,8 @@ def main():
     # out with it (its flush and exit); the other variants (no lines, the
     # remainder loops) do not run at R=64 n=7 (<= 16 pairs per step, nq % 4 == 0)
     loop_blocks = [b for b in order if sec_of[b].startswith("client loop")]
-    dots = {b: sum(1 for o in blk_ops[b] if o.startswith("v_dot2")) for b in loop_blocks}
-    big = [b for b in loop_blocks if dots[b] >= 16]
+    dots = {b: sum(1 for o in blk_ops[b] if o.startswith("v_dot2") or o.startswith("ds_add")) for b in loop_blocks}
+    big = [b for b in loop_blocks if dots[b] >= 8]
     hot = min(big, key=lambda b: sum(1 for o in blk_ops[b] if o.startswith("ds_"))) if big else None
     run = set()
     if hot:
@@ -94,7 +99,7 @@ def main():
         elif s in ("group precompute", "next group"):
             w = per_step_groups
         elif s.startswith("client loop"):
-            w = 4.0 if b == hot else (1.0 if b in run else 0.0)
+            w = float(trips) if b == hot else (1.0 if b in run else 0.0)
         else:
             w = 1.0
         for k, v in c.items():
@@ -127,8 +132,8 @@ def main():
     if pmc:
         meas = pmc["valu_insts_per_config"]
         # wavefront steps actually run per 64 configs: a group of C(p3, 3) configs takes ceil(/64) steps
-        from math import comb, ceil
-        ns, n = 64, 7
+        from math import ceil
+        ns = R
         real = sum(comb(ns - 1 - p3, n - 4) * ceil(comb(p3, 3) / 64) for p3 in range(3, ns)) / (comb(ns, n) / 64)
         print(f"Measured SQ_INSTS_VALU per 64 configs ({pmc['source']}): **{meas:.0f}**.  Groups run "
               f"{real:.3f} steps per 64 configs (partial last steps), so the model accounts for "
@@ -138,7 +143,8 @@ def main():
         ceil = 1.0 / (tot["valu_fast"] / model / FAST_RATE + (1 - tot["valu_fast"] / model) / SLOW_RATE) / 2.0
         print(f"Issue ceiling of this mix: {ceil:.1%} of the 2-cycle nominal rate; measured "
               f"{pmc['valu_issue_util']:.1%} ({pmc['valu_issue_util'] / ceil:.0%} of the ceiling).")
-    print(f"\nClient-loop hot body: `{hot}` ({len(blk_ops[hot]) if hot else 0} instructions for 4 quads = 16 clients).")
+    print(f"\nClient-loop hot body: `{hot}` ({len(blk_ops[hot]) if hot else 0} instructions per unrolled iteration, "
+          f"{trips} iterations per step).")
 
 
 if __name__ == "__main__":

@@ -8,13 +8,14 @@
 # Steps (outputs under gpurun_out/$TAG/):
 #   smoke    __graft_entry__.py (smoke on cuda:0)
 #   tests    pytest -m gpu over TEST_FILES (default tests/; PYTEST_EXPR: a -k expression)
-#   bench    bench.py with the CPU baseline, for each workload in WLS
+#   bench    bench.py with the CPU baseline, for each workload in BWLS (default WLS)
 #   ab       A/B timing of library variants: VARIANTS="default lib_x ..." (lib_x:
 #            fantoch_amd/lib_x/libbote_hip.so, scripts/build_variant.sh), REPS
 #            rounds interleaved, for each workload in WLS; AB_SKIP=1 passes
 #            --skip-fixture-check (diagnostics while a fixture is re-pinned)
 #   profile  rocprofv3 kernel trace + stats, then the PMC passes of
-#            scripts/summarize_profile.py, of bench.py on workload WL
+#            scripts/summarize_profile.py, of bench.py on each workload in
+#            PWLS (default WL), to gpurun_out/$TAG/<workload>/
 #   pmc      extra PMC passes: PASSES="ctr ...;ctr ..." over bench.py BENCH_ARGS
 #   shards   kernel trace of scripts/shard_ablate.py (per-dispatch cost of shards)
 #   ablate   scripts/ablate.py masks ABL on the -DBOTE_ABLATION library (lib_abl)
@@ -45,7 +46,7 @@ step_tests() {
 }
 
 step_bench() {
-  for wl in $WLS; do
+  for wl in ${BWLS:-$WLS}; do
     timeout -k 10 400 python -u bench.py --workload "$wl" --steps "${BSTEPS:-20}" --warmup 2 ${BENCH_ARGS:-} \
       > "$O/bench_$wl.log" 2>&1 || fail "bench $wl" $? "$O/bench_$wl.log"
     echo "bench $wl: $(grep -o '"ms_per_step": [0-9.]*\|"kernel_ms_avg": [0-9.]*\|"fixture": "[^"]*' "$O/bench_$wl.log" | tr '\n' ' ')"
@@ -70,18 +71,23 @@ step_ab() {
 
 step_profile() {
   export TMPDIR=/tmp
-  local B="python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --workload ${WL:-r64n7} ${BENCH_ARGS:-}"
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/trace" -o run -- $B \
-    > "$O/trace.log" 2>&1 || fail trace $? "$O/trace.log"
-  echo "trace ok"
-  local P1="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU"
-  local P2="SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_SMEM GRBM_GUI_ACTIVE GRBM_COUNT"
-  local i=0
-  for P in "$P1" "$P2" "FETCH_SIZE" "WRITE_SIZE"; do
-    i=$((i + 1))
-    timeout -s KILL 180 rocprofv3 --pmc $P --output-format csv -d "$O/pmc$i" -o run -- $B \
-      > "$O/pmc$i.log" 2>&1 || fail "pmc$i" $? "$O/pmc$i.log"
-    echo "pmc$i ok"
+  local wl
+  for wl in ${PWLS:-${WL:-r64n7}}; do
+    local P="$O/$wl"
+    mkdir -p "$P"
+    local B="python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --workload $wl ${BENCH_ARGS:-}"
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$P/trace" -o run -- $B \
+      > "$P/trace.log" 2>&1 || fail "trace $wl" $? "$P/trace.log"
+    echo "trace $wl ok"
+    local P1="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU"
+    local P2="SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_SMEM GRBM_GUI_ACTIVE GRBM_COUNT"
+    local i=0
+    for Q in "$P1" "$P2" "FETCH_SIZE" "WRITE_SIZE"; do
+      i=$((i + 1))
+      timeout -s KILL 240 rocprofv3 --pmc $Q --output-format csv -d "$P/pmc$i" -o run -- $B \
+        > "$P/pmc$i.log" 2>&1 || fail "pmc$i $wl" $? "$P/pmc$i.log"
+      echo "pmc$i $wl ok"
+    done
   done
 }
 
@@ -125,6 +131,13 @@ step_oracle() {
     --time-limit "${ORACLE_SECONDS:-600}" --state "$O/oracle_chunks.jsonl" > "$O/oracle.log" 2>&1 \
     || fail oracle $? "$O/oracle.log"
   echo "oracle: $(tail -1 "$O/oracle.log")"
+  if [ -n "${ORACLE_BEGIN2:-}" ]; then
+    timeout -k 10 $((${ORACLE_SECONDS2:-300} + 200)) python -u scripts/oracle_full_sweep.py --workload r64n7 \
+      --threads "${ORACLE_THREADS:-16}" --chunk 4194304 --partial --sweep-begin "$ORACLE_BEGIN2" \
+      --time-limit "${ORACLE_SECONDS2:-300}" --state "$O/oracle_chunks.jsonl" > "$O/oracle2.log" 2>&1 \
+      || fail oracle2 $? "$O/oracle2.log"
+    echo "oracle2: $(tail -1 "$O/oracle2.log")"
+  fi
 }
 
 for s in ${STEPS:?STEPS names the steps}; do

@@ -1,7 +1,7 @@
 """Summarise a `STEPS=profile` run of scripts/gpu_job.sh (gpurun_out/<TAG>/trace, pmc1..4) into
 profiles/<TAG>_profile.md and update profiles/traffic.json.
 
-  python scripts/summarize_profile.py r01 [workload_tag]
+  python scripts/summarize_profile.py r04d/r64n7 [workload_tag]   (the profile step's output directory)
 
 Per kernel: calls and average duration (rocprofv3 --kernel-trace --stats), then
 the per-dispatch PMC averages of each counter pass.  HBM traffic per launch of
@@ -109,13 +109,13 @@ def main():
                            "lds_insts_per_config": per.get("SQ_INSTS_LDS", 0) / lanes,
                            "salu_insts_per_config": per.get("SQ_INSTS_SALU", 0) / lanes,
                            "clock_ghz": clk, "kernel_ns": kns, "valu_issue_util": util,
-                           "source": f"profiles/{tag}_profile.md"}
+                           "source": f"profiles/{tag.replace('/', '_')}_profile.md"}
                 out.append(f"VALU wave-instructions per config: {pmc[wl]['valu_insts_per_config']:.1f} "
                            f"(LDS {pmc[wl]['lds_insts_per_config']:.1f}, SALU {pmc[wl]['salu_insts_per_config']:.1f}); "
                            f"VALU issue utilisation (SQ_INSTS_VALU x 2 cyc / (1024 SIMD x cycles) at "
                            f"{clk:.2f} GHz): {util:.1%}")
         out.append("")
-    open(os.path.join(ROOT, "profiles", f"{tag}_profile.md"), "w").write("\n".join(out) + "\n")
+    open(os.path.join(ROOT, "profiles", f"{tag.replace('/', '_')}_profile.md"), "w").write("\n".join(out) + "\n")
     if pmc:
         p = os.path.join(ROOT, "profiles", "pmc.json")
         d = json.load(open(p)) if os.path.exists(p) else {}

@@ -144,6 +144,27 @@ def test_r128n6_full_keys_group_equals_generic_on_a_slice():
     assert out["group"] == out["generic"]
 
 
+def test_r128n6_full_keys_group_equals_generic():
+    """BASELINE config 5 as stated at full size: all 5,423,611,200 configs of
+    R=128 n=6 with the extended key set, the group kernel (the bench path)
+    equal to the exact generic kernel -- every slot's and every leader's
+    moments through the digest, the valid count and the 8 objectives' top-K,
+    as the base key set's full sweep is checked in test_gpu_fixtures.py."""
+    p = Planet.synthetic(128)
+    dp = DevicePlanet(p)
+    srv = np.arange(128, dtype=np.uint32)
+    out = {}
+    for k in ("group", "generic"):
+        sw = Sweep(dp, srv, srv, 6, CONFIG5_OBJECTIVES, K=100, ranking=DEFAULT_RANKING, digest=True, kernel=k,
+                   keys=_lib.KEYS_TEMPO_ALL_LEADERS)
+        assert sw.kernel_path() == k
+        sw.launch(0, sw.total)
+        r = sw.result()
+        out[k] = (r.valid, r.digest, r.tops)
+    assert out["group"] == out["generic"]
+    assert out["group"][0] > 0 and all(len(t) == 100 for t in out["group"][2])
+
+
 def test_keys_argument_errors():
     p = Planet.new()
     dp = DevicePlanet(p)
