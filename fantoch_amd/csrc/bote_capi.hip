@@ -159,6 +159,7 @@ struct bote_sweep {
   // minima and the seed keys
   std::map<std::pair<uint64_t, uint64_t>, std::unique_ptr<Chunks>> samples;
   DBuf smin, tseed;
+  DBuf kbound;  // group lists' K-th key bound (FastArgs::kbound)
   // host walks of the groups (bote_host.hpp): one walk serves the split and
   // the chunk tables of every sub-range it covers (bote_search_* shares one
   // walk across its shards' sweeps)
@@ -1087,14 +1088,23 @@ static int sweep_chunks(bote_sweep* s, uint64_t rb, uint64_t re, hipStream_t st,
   return BOTE_OK;
 }
 
-// Merge `lists` per-block lists into the result block and append the counters.
+// Merge `lists` per-block lists into the result block and append the counters:
+// one launch when the group kernel bounded its lists (kbound: few records per
+// list), else the tree of 8-way merges (full lists).
 // With `sel` (fast path), the first level reads the overflow fallback's
 // `alt_lists` lists and counters instead when *sel > QUEUE_CAP (on the device).
+static bool wide_merge(uint32_t lists, uint32_t alt_lists) {
+  return lists <= bote::WIDE_MERGE_LISTS && alt_lists <= bote::WIDE_MERGE_LISTS;
+}
 static int merge_chain(bote_sweep* s, uint32_t lists, hipStream_t st, const unsigned long long* sel = nullptr,
-                       uint32_t alt_lists = 0) {
+                       uint32_t alt_lists = 0, const unsigned long long* kbound = nullptr) {
   const uint64_t lstride = (uint64_t)s->n_obj * bote::KP;
   Rec* rec_out = s->result.as<Rec>();
-  if (s->n_obj) {
+  if (s->n_obj && kbound && wide_merge(lists, alt_lists)) {
+    // one launch: the lists' filled prefixes gathered and sorted in LDS
+    HIP_TRY(bote::launch_merge_wide(s->top.as<Rec>(), lists, s->top_alt.as<Rec>(), sel ? alt_lists : 0, lstride, sel,
+                                    QUEUE_CAP, kbound, rec_out, s->n_obj, s->K, st));
+  } else if (s->n_obj) {
     const Rec* src = s->top.as<Rec>();
     Rec* bufs[2] = {s->tmp0.as<Rec>(), s->tmp1.as<Rec>()};
     int b = 0;
@@ -1160,6 +1170,9 @@ static int launch_generic(bote_sweep* s, uint64_t rb, uint64_t re, hipStream_t s
 
 // The top-K seed of a group launch over [rb, re) (launch_fast_path): sets
 // f.tseed, or leaves it null when the range is too small to sample.
+#ifndef BOTE_SEED_PER_WAVE
+#define BOTE_SEED_PER_WAVE 1  // sample minima per wave (4,096 slots) instead of per chunk (32,768)
+#endif
 #ifndef BOTE_SEED_STEPS
 #define BOTE_SEED_STEPS 8  // sample steps per wave (r03v A/B: 8 vs 1, kernel -1.6 %, 1/8 shard -5 %)
 #endif
@@ -1208,9 +1221,12 @@ static int sample_seed(bote_sweep* s, bote::FastArgs& f, uint64_t rb, uint64_t r
     it = s->samples.emplace(key, std::move(c)).first;
   }
   const bote_sweep::Chunks* c = it->second.get();
-  if (s->smin.reserve((size_t)s->n_obj * nsamp * 8) != hipSuccess || s->tseed.reserve(bote::MAXOBJ * 8) != hipSuccess)
+  // slots: one per wave (BOTE_SEED_PER_WAVE) or one per chunk
+  const uint32_t slots = BOTE_SEED_PER_WAVE && nwaves >= s->K ? nwaves : nsamp;
+  if (s->smin.reserve((size_t)s->n_obj * slots * 8) != hipSuccess || s->tseed.reserve(bote::MAXOBJ * 8) != hipSuccess)
     return fail(BOTE_E_NOMEM, "hipMalloc top-K seed");
-  HIP_TRY(hipMemsetAsync(s->smin.p, 0xFF, (size_t)s->n_obj * nsamp * 8, st));
+  // (per-wave slots: each wave clears its own at the sample launch's start)
+  if (slots != nwaves || slots == nsamp) HIP_TRY(hipMemsetAsync(s->smin.p, 0xFF, (size_t)s->n_obj * slots * 8, st));
   bote::FastArgs fs = f;
   fs.smin = s->smin.as<uint64_t>();
   fs.tseed = nullptr;
@@ -1218,9 +1234,10 @@ static int sample_seed(bote_sweep* s, bote::FastArgs& f, uint64_t rb, uint64_t r
   fs.wstate = c->sdev.as<uint64_t>();
   fs.nwchunks = nsamp;
   fs.ssteps = ssteps;
+  fs.smin_wave = slots == nwaves && slots != nsamp ? 1u : 0u;
   fs.wctr = f.wctr + 256;  // the sample launch's ticket shards
   HIP_TRY(bote::launch_group(fs, s->n, s->def_obj, s->fgrid, s->fshm, st));
-  HIP_TRY(bote::launch_seed(fs.smin, nsamp, s->n_obj, s->K, s->tseed.as<uint64_t>(), st));
+  HIP_TRY(bote::launch_seed(fs.smin, fs.smin_wave ? nwaves : nsamp, s->n_obj, s->K, s->tseed.as<uint64_t>(), st));
   f.tseed = s->tseed.as<uint64_t>();
   return BOTE_OK;
 }
@@ -1250,8 +1267,15 @@ static int launch_fast_path(bote_sweep* s, uint64_t rb, uint64_t re, hipStream_t
     }
   }
   // counters, deferred count, work tickets, fallback counters: one launch
+  // the group blocks' lists shrink to the records within the least K-th key
+  // of any block's list when the one-launch merge reads them
+  f.kbound = nullptr;
+  if (s->group && s->n_obj && s->K && wide_merge(s->fgrid + s->xgrid, s->grid)) {
+    if (!s->kbound.p && s->kbound.alloc(bote::MAXOBJ * 8) != hipSuccess) return fail(BOTE_E_NOMEM, "hipMalloc K-th key bound");
+    f.kbound = s->kbound.as<unsigned long long>();
+  }
   HIP_TRY(bote::launch_zero_ctl(s->counters.as<unsigned long long>(), s->qcount.as<unsigned long long>(),
-                                f.nwchunks ? f.wctr : nullptr, s->counters_alt.as<unsigned long long>(), st));
+                                f.nwchunks ? f.wctr : nullptr, s->counters_alt.as<unsigned long long>(), f.kbound, st));
   // top-K seed: one step of 64 configs per wave at evenly spaced ranks, then
   // per objective the K-th least of the chunks' minimum keys (a bound on the
   // range's K-th key: K distinct configs of the range reach it), so that the
@@ -1294,7 +1318,7 @@ static int launch_fast_path(bote_sweep* s, uint64_t rb, uint64_t re, hipStream_t
   g.run_if_over = s->qcount.as<unsigned long long>();
   g.over_cap = QUEUE_CAP;
   HIP_TRY(bote::launch_eval(g, s->n, false, s->grid, s->bd, s->shm, st));
-  return merge_chain(s, s->fgrid + s->xgrid, st, s->qcount.as<unsigned long long>(), s->grid);
+  return merge_chain(s, s->fgrid + s->xgrid, st, s->qcount.as<unsigned long long>(), s->grid, f.kbound);
 }
 
 int bote_sweep_launch(bote_sweep* s, uint64_t rank_begin, uint64_t rank_end, void* hip_stream) {

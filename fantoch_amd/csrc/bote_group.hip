@@ -369,10 +369,7 @@ __device__ __forceinline__ float u64_to_f32(uint64_t x) {
 // VGPRs); config 5 (R = 128) is LDS-bound at 3 workgroups per CU anyway.
 // (a 1024-thread bound would cap registers at 128 whatever the wave target:
 // the XK kernels are bounded to 768-thread workgroups, 3 waves per SIMD each)
-#ifndef BOTE_GROUP_WAVES_XK
-#define BOTE_GROUP_WAVES_XK 3
-#endif
-// (GROUP_XK_MAX_BD = 768: bote_kernels.hpp)
+// (BOTE_GROUP_WAVES_XK, GROUP_XK_MAX_BD = 256 x that: bote_kernels.hpp)
 // client-loop quads per iteration of the base kernels (a build knob)
 #ifndef BOTE_GROUP_UNROLL
 #define BOTE_GROUP_UNROLL 4
@@ -446,6 +443,11 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
   // objective's K-th key over the launch range, from the sample launch)
   if (tid < MAXOBJ) tk.thr[tid] = a.tseed && tid < a.n_obj ? Rec{a.tseed[tid], ~0ull} : rec_max();
   if (tid == 0) *lock = 0;
+  // sample launch with a slot per wave: lane o clears the wave's slot of
+  // objective o (no memset before the launch); the same lane's atomicMin
+  // per chunk follows it in program order
+  if (a.smin && a.smin_wave && lane < a.n_obj)
+    a.smin[(size_t)lane * gridDim.x * WPB + (size_t)blockIdx.x * WPB + wid] = ~0ull;
   // BIN: the member bins start at zero (each lane re-zeroes its own after use)
   if constexpr (BIN)
     for (uint32_t i = tid; i < (BD >> 6) * N * 64; i += BD) ((uint32_t*)(smem + off[14]))[i] = 0;
@@ -1318,7 +1320,9 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
                 };
                 auto clients_bin = [&](auto lines_c) {
                   // s2l (squared keys) is flushed to 64 bits every k_flush quads
-                  constexpr uint32_t UB = 4;
+                  // (4 quads per iteration; 2 without lines, whose 4 sources
+                  // per pair of quads would hold 32 VGPRs of reads at 4)
+                  constexpr uint32_t UB = decltype(lines_c)::value ? 4u : 2u;
                   const uint32_t fU = a.k_flush / UB ? a.k_flush / UB : 1u;
                   uint32_t g = 0, k = 0;
                   if (a.k_flush >= UB) {
@@ -1674,7 +1678,10 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
                                  (uint32_t)__shfl_xor((int)(uint32_t)v, d);
               v = w < v ? w : v;
             }
-            if (lane == 0 && v != ~0ull) atomicMin((unsigned long long*)&a.smin[(size_t)o * a.nwchunks + chunk], v);
+            const size_t slot = a.smin_wave ? (size_t)o * gridDim.x * WPB + (size_t)blockIdx.x * WPB + wid
+                                            : (size_t)o * a.nwchunks + chunk;
+            if (lane == (a.smin_wave ? (uint32_t)o : 0u) && v != ~0ull)
+              atomicMin((unsigned long long*)&a.smin[slot], v);
           }
         } else if (!ABLATE(a, 4)) {
           const int nobj = XK ? 8 : (DEF ? 5 : a.n_obj);
@@ -1721,6 +1728,38 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
   if (digest) atomicAdd(&a.out_counters[1], (unsigned long long)digest);
   __syncthreads();
   Rec* dst = a.out_top + (size_t)blockIdx.x * a.n_obj * KP;
+  if (a.kbound) {
+    // the one-launch merge follows: publish this list's K-th key (a bound on
+    // the union's K-th key), then write only the records within the least
+    // bound seen so far and a terminator (tk.thr is free now: its key holds
+    // the bound)
+    if (tid < a.n_obj) {
+      const Rec kth = tk.top[tid * a.K + a.K - 1];
+      uint64_t b = ~0ull;
+      if (!(kth.key == ~0ull && kth.rank == ~0ull)) {
+        b = atomicMin(&a.kbound[tid], (unsigned long long)kth.key);  // (vector atomic)
+        b = b < kth.key ? b : kth.key;
+      } else {
+        b = __hip_atomic_load(&a.kbound[tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      tk.thr[tid].key = b;
+    }
+    __syncthreads();
+    for (uint32_t i = tid; i < (uint32_t)a.n_obj * a.K; i += BD) {
+      const uint32_t o = i / a.K, e = i % a.K;
+      const uint64_t b = tk.thr[o].key;
+      const Rec r = tk.top[i];
+      const bool in = !(r.key == ~0ull && r.rank == ~0ull) && r.key <= b;
+      bool prev = true;
+      if (e) {
+        const Rec q = tk.top[i - 1];
+        prev = !(q.key == ~0ull && q.rank == ~0ull) && q.key <= b;
+      }
+      if (in) dst[o * KP + e] = r;
+      else if (prev) dst[o * KP + e] = rec_max();  // the terminator
+    }
+    return;
+  }
   for (uint32_t i = tid; i < (uint32_t)a.n_obj * KP; i += BD) {
     const uint32_t o = i / KP, e = i % KP;
     dst[i] = e < a.K ? tk.top[o * a.K + e] : rec_max();

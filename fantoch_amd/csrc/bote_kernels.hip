@@ -17,6 +17,7 @@
 //   rank enumeration       Search::compute_configs fantoch_bote/src/search.rs:234-260
 //                          (permutator combination -> colex ranks)
 //   k_single_*             Bote::{leaderless, leader, all_leaders_stats, best_leader}
+#include <atomic>
 #include "bote_kernels.hpp"
 
 namespace bote {
@@ -781,6 +782,145 @@ hipError_t launch_merge_sel(const Rec* src, uint32_t n_lists, const Rec* alt, ui
   return hipGetLastError();
 }
 
+// ------------------------------------------------- one-launch list merge --
+// The per-block top-K lists of a sweep launch are mostly padding: after the
+// seed (bote_capi.hip sample_seed) a block list holds only the records that
+// beat a bound on the launch's K-th key, ~0-2 per objective.  One workgroup
+// per objective gathers the lists' filled prefixes (records before the first
+// rec_max) into LDS and sorts them with the running K least; lists whose
+// records do not fit one pass (WIDE_CAP) are taken in further passes, so the
+// result is the K least of the union whatever the fill (deterministic: the
+// (key, rank) order is total).  Replaces the 4-level merge_kernel tree of a
+// sweep's 1,024+ lists (one launch instead of four).
+constexpr int WIDE_BD = 1024, WIDE_SORT = 4096, WIDE_LISTS_PER_THREAD = 4, WIDE_HEAD = 4;
+__device__ __forceinline__ bool is_rec_max(const Rec& r) { return r.key == ~0ull && r.rank == ~0ull; }
+static_assert(WIDE_MERGE_LISTS == (uint32_t)(WIDE_BD * WIDE_LISTS_PER_THREAD), "one thread per WIDE_LISTS_PER_THREAD lists");
+size_t merge_wide_smem() { return (size_t)WIDE_SORT * sizeof(Rec) + (WIDE_BD + 8) * sizeof(uint32_t); }
+
+__global__ void __launch_bounds__(WIDE_BD) merge_wide_kernel(const Rec* src, uint32_t n_lists, uint64_t list_stride,
+                                                             Rec* dst, const Rec* alt, uint32_t alt_lists,
+                                                             const unsigned long long* sel, uint64_t cap,
+                                                             const unsigned long long* kbound, uint32_t K) {
+  const bool use_alt = sel && *sel > cap;
+  if (use_alt) {  // device-side choice of the input (fast sweep overflow fallback)
+    src = alt;
+    n_lists = alt_lists;
+  }
+  extern __shared__ __align__(16) unsigned char wsm[];
+  Rec* buf = (Rec*)wsm;
+  uint32_t* scan = (uint32_t*)(wsm + (size_t)WIDE_SORT * sizeof(Rec));
+  uint32_t* ctl = scan + WIDE_BD;  // [0] next window start, [1] records this pass
+  const uint32_t o = blockIdx.x, tid = threadIdx.x;
+  const uint32_t KK = K < (uint32_t)KP ? K : (uint32_t)KP;
+  // records above the bound on the K-th key (the least K-th key of the
+  // group blocks' full lists) cannot be among the K least of the union
+  const uint64_t bound = kbound && !use_alt ? kbound[o] : ~0ull;
+  auto keep = [&](const Rec& r) { return !is_rec_max(r) && r.key <= bound; };
+  // per list: the filled prefix length (a sorted list padded with rec_max);
+  // the first WIDE_HEAD records of all of a thread's lists load together
+  constexpr int H = WIDE_HEAD;
+  Rec head[WIDE_LISTS_PER_THREAD][H];
+  uint32_t cnt[WIDE_LISTS_PER_THREAD], off[WIDE_LISTS_PER_THREAD], mine = 0;
+#pragma unroll
+  for (int j = 0; j < WIDE_LISTS_PER_THREAD; ++j) {
+    const uint32_t l = tid * WIDE_LISTS_PER_THREAD + j;
+    const Rec* L = src + (size_t)l * list_stride + o * KP;
+#pragma unroll
+    for (int c = 0; c < H; ++c) head[j][c] = l < n_lists && (uint32_t)c < KK ? L[c] : rec_max();
+  }
+#pragma unroll
+  for (int j = 0; j < WIDE_LISTS_PER_THREAD; ++j) {
+    uint32_t c = 0;
+#pragma unroll
+    for (int i = 0; i < H; ++i) c += (uint32_t)(c == (uint32_t)i && keep(head[j][i]));
+    if (c == (uint32_t)H) {  // a long list (rare): walk the rest
+      const Rec* L = src + (size_t)(tid * WIDE_LISTS_PER_THREAD + j) * list_stride + o * KP;
+      while (c < KK && keep(L[c])) ++c;
+    }
+    cnt[j] = c;
+    off[j] = mine;
+    mine += c;
+  }
+  // exclusive scan of the threads' totals (list order = thread order)
+  scan[tid] = mine;
+  __syncthreads();
+  for (uint32_t d = 1; d < WIDE_BD; d <<= 1) {
+    const uint32_t v = tid >= d ? scan[tid - d] : 0u;
+    __syncthreads();
+    scan[tid] += v;
+    __syncthreads();
+  }
+  const uint32_t base = scan[tid] - mine;  // records before this thread's lists
+#pragma unroll
+  for (int j = 0; j < WIDE_LISTS_PER_THREAD; ++j) off[j] += base;
+  const uint32_t total = scan[WIDE_BD - 1];
+  // running K least: buf[0 .. have)
+  uint32_t have = 0;
+  const uint32_t room = WIDE_SORT - KK;  // records gathered per pass
+  uint32_t w0 = 0;  // window start (in the concatenated order)
+  while (w0 < total) {
+    __syncthreads();
+    if (tid == 0) {
+      ctl[0] = total;  // the next window starts at the first list that does not fit
+      ctl[1] = 0;
+    }
+    __syncthreads();
+    // lists inside [w0, w0 + room) are copied after the running list
+#pragma unroll
+    for (int j = 0; j < WIDE_LISTS_PER_THREAD; ++j) {
+      const uint32_t l = tid * WIDE_LISTS_PER_THREAD + j;
+      if (cnt[j] == 0 || off[j] < w0) continue;
+      if (off[j] + cnt[j] - w0 <= room) {
+        Rec* d = buf + KK + off[j] - w0;
+#pragma unroll
+        for (int c = 0; c < H; ++c)
+          if ((uint32_t)c < cnt[j]) d[c] = head[j][c];
+        const Rec* L = src + (size_t)l * list_stride + o * KP;
+        for (uint32_t c = H; c < cnt[j]; ++c) d[c] = L[c];
+        atomicMax(&ctl[1], off[j] + cnt[j] - w0);
+      } else {
+        atomicMin(&ctl[0], off[j]);
+      }
+    }
+    __syncthreads();
+    const uint32_t got = ctl[1], next = ctl[0];
+    // compact: running records at [0, have), the pass's at [KK, KK + got)
+    uint32_t n = KK + got, P = 2;
+    while (P < n) P <<= 1;
+    for (uint32_t i = tid; i < P; i += WIDE_BD)
+      if ((i >= have && i < KK) || i >= n) buf[i] = rec_max();
+    __syncthreads();
+    block_bitonic(buf, (int)P);
+    have = min(KK, n);
+    w0 = next;
+  }
+  __syncthreads();
+  Rec* out = dst + o * KP;
+  for (uint32_t i = tid; i < (uint32_t)KP; i += WIDE_BD) out[i] = i < have && i < KK ? buf[i] : rec_max();
+}
+
+hipError_t launch_merge_wide(const Rec* src, uint32_t n_lists, const Rec* alt, uint32_t alt_lists, uint64_t list_stride,
+                             const unsigned long long* sel, uint64_t cap, const unsigned long long* kbound, Rec* dst,
+                             uint32_t n_obj, uint32_t K, hipStream_t st) {
+  if (n_lists > (uint32_t)(WIDE_BD * WIDE_LISTS_PER_THREAD) || alt_lists > (uint32_t)(WIDE_BD * WIDE_LISTS_PER_THREAD))
+    return hipErrorInvalidValue;
+  const size_t shm = merge_wide_smem();
+  // (the LDS limit above 64 KB, once per device)
+  static std::atomic<uint64_t> done{0};
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  const uint64_t bit = 1ull << (dev & 63);
+  if (!(done.load(std::memory_order_relaxed) & bit)) {
+    e = hipFuncSetAttribute((const void*)merge_wide_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
+    if (e != hipSuccess) return e;
+    done.fetch_or(bit, std::memory_order_relaxed);
+  }
+  hipLaunchKernelGGL(merge_wide_kernel, dim3(n_obj), dim3(WIDE_BD), shm, st, src, n_lists, list_stride, dst, alt,
+                     alt_lists, sel, cap, kbound, K);
+  return hipGetLastError();
+}
+
 __global__ void pick_counters_kernel(const unsigned long long* src, const unsigned long long* alt,
                                      const unsigned long long* sel, uint64_t cap, uint64_t* dst) {
   if (threadIdx.x < 2) dst[threadIdx.x] = (*sel > cap ? alt : src)[threadIdx.x];
@@ -790,17 +930,18 @@ __global__ void pick_counters_kernel(const unsigned long long* src, const unsign
 // (valid/digest counters, the deferred-queue count, the work-ticket counter,
 // the overflow fallback's counters) instead of four memsets
 __global__ void zero_ctl_kernel(unsigned long long* counters, unsigned long long* qcount, unsigned int* wctr,
-                                unsigned long long* counters_alt) {
+                                unsigned long long* counters_alt, unsigned long long* kbound) {
   const uint32_t t = threadIdx.x;
   if (t < 2) counters[t] = 0;
   if (t == 2) *qcount = 0;
   if (t >= 4 && t < 6) counters_alt[t - 4] = 0;
   if (t >= 8 && t < 24 && wctr) wctr[32 * (t - 8)] = 0;  // the 8 ticket-counter shards, main and sample launch
+  if (t >= 32 && t < 32 + MAXOBJ && kbound) kbound[t - 32] = ~0ull;  // the lists' K-th key bound (no bound)
 }
 
 hipError_t launch_zero_ctl(unsigned long long* counters, unsigned long long* qcount, unsigned int* wctr,
-                           unsigned long long* counters_alt, hipStream_t st) {
-  hipLaunchKernelGGL(zero_ctl_kernel, dim3(1), dim3(64), 0, st, counters, qcount, wctr, counters_alt);
+                           unsigned long long* counters_alt, unsigned long long* kbound, hipStream_t st) {
+  hipLaunchKernelGGL(zero_ctl_kernel, dim3(1), dim3(64), 0, st, counters, qcount, wctr, counters_alt, kbound);
   return hipGetLastError();
 }
 

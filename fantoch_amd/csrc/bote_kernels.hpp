@@ -124,9 +124,18 @@ struct FastArgs {
   // counters or deferrals); seed_kernel turns those into tseed[o], the K-th
   // least, a bound on the launch's K-th key that the main launch starts its
   // thresholds at
+  // With smin_wave, the slot is the wave's (o * waves + wave, the least key
+  // of the chunks it took): as many slots as waves, not chunks, for the seed
+  // kernel to select from (K slots <= x are still K distinct configs <= x).
   uint64_t* smin;
   const uint64_t* tseed;
   uint32_t ssteps;  // sample launch: steps (of 64 configs) per sample chunk
+  uint32_t smin_wave;
+  // kbound (non-null: the one-launch merge follows): per objective the least
+  // K-th key over the blocks' full lists (atomicMin at the list dump, reset by
+  // zero_ctl); a block then writes only its records with keys <= that bound,
+  // then a rec_max terminator, instead of n_obj x KP records
+  unsigned long long* kbound;
   int want_score, p_int;
   int64_t p1i, p2i;  // p_int: min_mean_{fpaxos,epaxos}_improv * nc as integers
   // group kernel mean tests on D = the integer difference of two sums: true
@@ -207,7 +216,12 @@ bool group_uses_lines(uint32_t n);  // n <= 7: client lines (FastArgs::gslots) a
 // the extended key set's group kernels are bounded to this workgroup size (3
 // waves per SIMD at <= 168 VGPRs; bote_group.hip); the capi's eligibility
 // probe and its geometry loop share it
-constexpr uint32_t GROUP_XK_MAX_BD = 768;
+// the extended key set's kernels: BOTE_GROUP_WAVES_XK waves per SIMD (3:
+// <= 168 VGPRs), so workgroups of at most that many waves per SIMD
+#ifndef BOTE_GROUP_WAVES_XK
+#define BOTE_GROUP_WAVES_XK 3
+#endif
+constexpr uint32_t GROUP_XK_MAX_BD = 256 * BOTE_GROUP_WAVES_XK;
 bool group_supports_keys(uint32_t n, uint32_t bd);  // the extended key set on the group kernel (n = 4..7, bd <= GROUP_XK_MAX_BD)
 // workgroups per CU of the kernel instantiation launch_group runs for `a`
 // (workgroup size a.gbd)
@@ -222,12 +236,18 @@ hipError_t launch_merge(const Rec* src, uint32_t n_lists, uint64_t list_stride, 
                         uint32_t n_obj, hipStream_t st);
 // Merge whose input is chosen on the device: `alt` (alt_lists lists) when
 // *sel > cap, else `src` (n_lists lists).
+constexpr uint32_t WIDE_MERGE_LISTS = 4096;
+// one launch for a sweep's block lists (<= WIDE_MERGE_LISTS lists): the K least per
+// objective into dst[o * KP] (sel/alt/cap: the overflow fallback's choice)
+hipError_t launch_merge_wide(const Rec* src, uint32_t n_lists, const Rec* alt, uint32_t alt_lists, uint64_t list_stride,
+                             const unsigned long long* sel, uint64_t cap, const unsigned long long* kbound, Rec* dst,
+                             uint32_t n_obj, uint32_t K, hipStream_t st);
 hipError_t launch_merge_sel(const Rec* src, uint32_t n_lists, const Rec* alt, uint32_t alt_lists, uint64_t list_stride,
                             const unsigned long long* sel, uint64_t cap, Rec* dst, uint64_t out_stride, uint32_t n_obj,
                             hipStream_t st);
 // dst[0..1] = (*sel > cap ? alt : src)[0..1]
 hipError_t launch_zero_ctl(unsigned long long* counters, unsigned long long* qcount, unsigned int* wctr,
-                           unsigned long long* counters_alt, hipStream_t st);
+                           unsigned long long* counters_alt, unsigned long long* kbound, hipStream_t st);
 hipError_t launch_seed(const uint64_t* smin, uint32_t nsamp, uint32_t n_obj, uint32_t K, uint64_t* tseed,
                        hipStream_t st);
 hipError_t launch_pick_counters(const unsigned long long* src, const unsigned long long* alt,

@@ -77,10 +77,27 @@ def main():
     # remainder loops) do not run at R=64 n=7 (<= 16 pairs per step, nq % 4 == 0)
     loop_blocks = [b for b in order if sec_of[b].startswith("client loop")]
     dots = {b: sum(1 for o in blk_ops[b] if o.startswith("v_dot2") or o.startswith("ds_add")) for b in loop_blocks}
+    adds = {b: sum(1 for o in blk_ops[b] if o.startswith("ds_add")) for b in loop_blocks}
     big = [b for b in loop_blocks if dots[b] >= 8]
+    if any(adds[b] >= 8 for b in loop_blocks):
+        # the member-binned loop (BIN kernels): its bodies are the blocks of
+        # LDS adds (the epilogue after it has the most v_dot2 but runs once)
+        big = [b for b in loop_blocks if adds[b] >= 8]
     hot = min(big, key=lambda b: sum(1 for o in blk_ops[b] if o.startswith("ds_"))) if big else None
     run = set()
-    if hot:
+    if hot and any(adds[b] >= 8 for b in loop_blocks):
+        # BIN: once per step, the blocks between the lines body and the next
+        # loop body (its flush and exit), and the epilogue over the bins (the
+        # client-loop block without LDS adds that has the most v_dot2)
+        i = order.index(hot) + 1
+        while i < len(order) and not (order[i] in big):
+            if sec_of[order[i]].startswith("client loop") and adds[order[i]] == 0:
+                run.add(order[i])
+            i += 1
+        tail = [b for b in loop_blocks if adds[b] == 0]
+        if tail:
+            run.add(max(tail, key=lambda b: sum(1 for o in blk_ops[b] if o.startswith("v_dot2"))))
+    elif hot:
         i = order.index(hot)
         while i < len(order) and sec_of[order[i]].startswith("client loop"):
             run.add(order[i])
@@ -99,7 +116,9 @@ def main():
         elif s in ("group precompute", "next group"):
             w = per_step_groups
         elif s.startswith("client loop"):
-            w = float(trips) if b == hot else (1.0 if b in run else 0.0)
+            # (the other variants' bodies and the remainder loops: 0)
+            other_body = b != hot and (adds[b] > 0 or b in big)
+            w = float(trips) if b == hot else (1.0 if b in run and not other_body else 0.0)
         else:
             w = 1.0
         for k, v in c.items():
