@@ -102,3 +102,28 @@ def test_bound_is_no_tighter_than_the_union_kth_key():
     _, bound = dump(lists, K, list(range(50)))
     union = sorted(r for L in lists for r in L)[:K]
     assert union[-1][0] <= bound
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_per_wave_sample_minima_bound_the_kth_key(seed):
+    """The top-K seed (bote_capi.hip sample_seed, FastArgs::smin_wave): each
+    wave's slot is the least key over the chunks it took, and the seed is the
+    K-th least slot (all-ones when fewer than K slots hold a key).  K slots at
+    or below the seed are K distinct configs of the range, so the seed is an
+    upper bound on the range's K-th key."""
+    rng = random.Random(100 + seed)
+    K = rng.choice([1, 5, 100])
+    waves = rng.choice([64, 300, 4096])
+    chunks = [[rng.randrange(10**4) for _ in range(rng.randrange(0, 64))] for _ in range(waves * 8)]
+    slots = [2**64 - 1] * waves
+    order = list(range(len(chunks)))
+    rng.shuffle(order)  # tickets: any wave may take any chunk
+    for i, c in enumerate(order):
+        w = i % waves
+        if chunks[c]:
+            slots[w] = min(slots[w], min(chunks[c]))
+    # (seed_kernel: all-ones, no bound, with fewer than K slots)
+    seed_key = sorted(slots)[K - 1] if waves >= K else 2**64 - 1
+    every = sorted(k for ch in chunks for k in ch)
+    if len(every) >= K and seed_key != 2**64 - 1:
+        assert every[K - 1] <= seed_key
