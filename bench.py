@@ -263,6 +263,19 @@ def load_fixture(workload):
     return json.load(open(p)) if os.path.exists(p) else None
 
 
+def lib_build():
+    """Identity of the loaded product library: the first 16 hex digits of the
+    sha256 of its file (fantoch_amd/lib/libbote_hip.so, or BOTE_LIB_PATH).
+    Profile-derived figures (profiles/pmc.json, traffic.json) carry the build
+    they were measured on, and the line quotes them only for the same build."""
+    import hashlib
+
+    from fantoch_amd import _lib
+
+    with open(_lib.LIB_PATH, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()[:16]
+
+
 def load_pmc(tag):
     """Per-workload PMC figures committed under profiles/pmc.json
     (scripts/summarize_profile.py): VALU instructions per config-lane etc."""
@@ -276,13 +289,42 @@ def load_pmc(tag):
 
 
 def load_traffic(tag):
+    """HBM bytes per launch of the sweep kernel (profiles/traffic.json):
+    {"bytes": B, "build": lib_build() of the profiled library, "source": ...}."""
     p = os.path.join(ROOT, "profiles", "traffic.json")
     if os.path.exists(p):
         try:
-            return json.load(open(p)).get(tag)
+            t = json.load(open(p)).get(tag)
         except Exception:
             return None
+        return t if isinstance(t, dict) else None
     return None
+
+
+def profile_figures(pmc, traffic, build, shard, kavg_ms):
+    """The line's profile-derived fields: VALU issue utilisation from the
+    PMC instruction count and this run's kernel time, and the HBM traffic per
+    launch -- each only when it was measured on this very build (ADVICE r04:
+    a count from another build is not evidence for this one)."""
+    valu, stale = None, []
+    if pmc and pmc.get("valu_insts_per_config"):
+        insts = pmc["valu_insts_per_config"] * shard / 64
+        clk = pmc.get("clock_ghz", 2.4)
+        same = pmc.get("build") == build
+        valu = {"insts_per_config": pmc["valu_insts_per_config"], "clock_ghz": clk,
+                # SQ_INSTS_VALU x 2 cycles (a wave64 VALU op issues over 2 cycles on a
+                # SIMD-32) over SIMD-cycles of the live kernel time at the PMC run's clock
+                "util": insts * 2 / (1024 * kavg_ms * 1e-3 * clk * 1e9) if same else None,
+                "source": pmc.get("source"), "pmc_build": pmc.get("build"), "same_build": same}
+        if not same:
+            stale.append(f"valu_issue: profiles/pmc.json was measured on build {pmc.get('build')}, not {build}")
+    tb = None
+    if traffic:
+        if traffic.get("build") == build:
+            tb = traffic.get("bytes")
+        else:
+            stale.append(f"traffic: profiles/traffic.json was measured on build {traffic.get('build')}, not {build}")
+    return valu, tb, stale
 
 
 def main():
@@ -421,18 +463,10 @@ def main():
         Wg = work_per_config_keys(n, planet.R) if wl["keys"] else work_per_config_group(n, planet.R)
         shard = e - b
         achieved = shard * Wg / (kavg_ms * 1e-3) / 1e12  # T int-ops/s of W', dominant kernel
-        traffic = load_traffic(f"{args.workload}_n{world}")
+        build = lib_build()
         grid, block, lds = sweep.geometry()
-        pmc = load_pmc(f"{args.workload}_n1")
-        valu = None
-        if pmc and pmc.get("valu_insts_per_config"):
-            # SQ_INSTS_VALU x 2 cycles (a wave64 VALU op issues over 2 cycles on a
-            # SIMD-32) over SIMD-cycles of the live kernel time at the PMC run's clock
-            insts = pmc["valu_insts_per_config"] * shard / 64
-            clk = pmc.get("clock_ghz", 2.4)
-            valu = {"insts_per_config": pmc["valu_insts_per_config"], "clock_ghz": clk,
-                    "util": insts * 2 / (1024 * kavg_ms * 1e-3 * clk * 1e9), "source": pmc.get("source"),
-                    "pmc_build": pmc.get("build")}
+        valu, traffic, stale = profile_figures(load_pmc(f"{args.workload}_n1"),
+                                               load_traffic(f"{args.workload}_n{world}"), build, e - b, kavg_ms)
         out = {
             "metric": METRIC if args.workload == "r64n7" else f"region configs evaluated/sec, {wl['desc']}",
             "value": total * args.steps / dt,
@@ -441,6 +475,9 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": dt / args.steps * 1e3,
+            # per-step time outside the sweep kernel: zeroing, sample launch,
+            # seed, fix-up, merge, result copy (and the all-gather at N > 1)
+            "step_overhead_ms": dt / args.steps * 1e3 - kavg_ms,
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
@@ -450,7 +487,7 @@ def main():
                        "keys": 20 if wl["keys"] else 10, "key_set": wl["keys"], "objectives": len(objectives),
                        "K": 100,
                        "parallelism": f"rank-shard x{world}", "grid": grid, "block": block, "lds_bytes": lds,
-                       "kernel_path": sweep.kernel_path()},
+                       "kernel_path": sweep.kernel_path(), "lib_build": build},
             "roofline": {"bound": "valu", "achieved": achieved, "peak": VALU_PEAK_TOPS, "unit": "Tops/s",
                          "frac": achieved / VALU_PEAK_TOPS, "traffic": traffic,
                          "work_per_config": Wg,
@@ -461,6 +498,7 @@ def main():
                          # SIMD-cycles); frac above is W' (algorithmic ops) over the lane-op peak and runs
                          # above issue where W' overcounts the executed instructions (R=128)
                          "util": valu["util"] if valu else None,
+                         "stale": stale or None,
                          "util_def": "VALU issue: SQ_INSTS_VALU x 2 cycles / (1024 SIMDs x kernel cycles), "
                                      "profiles/pmc.json",
                          "frac_vs_util": (achieved / VALU_PEAK_TOPS) / valu["util"] if valu and valu["util"] else None,

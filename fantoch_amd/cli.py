@@ -64,8 +64,11 @@ def distance_table(planet, regions: Sequence[str]) -> str:
     return planet.distance_matrix([Region(r) for r in regions])
 
 
-def best_chains(args, out=sys.stdout) -> None:
-    """main.rs:32-85 (the search, then the best chain's score and stats)."""
+def best_chains(args, out=sys.stdout) -> int:
+    """main.rs:32-85 (the search, then the best chain's score and stats).
+    main.rs takes the best chain with `.next().unwrap()`, which panics (exit
+    101) when no evolving chain exists: with no chain this prints an error to
+    stderr and returns 101."""
     from .bote import FTMetric, RankingParams, Search, SearchInput
 
     planet = _planet(args)
@@ -74,6 +77,9 @@ def best_chains(args, out=sys.stdout) -> None:
     a, b, c, d = (int(x) for x in args.ranking.split(","))
     params = RankingParams.new(a, b, c, d, args.min_n, args.max_n, FTMetric[args.ft_metric])
     chains = search.sorted_evolving_configs(params, limit=args.chains)
+    if not chains:
+        print("error: no evolving config chain (main.rs:66-69 `.next().unwrap()` on None)", file=sys.stderr)
+        return 101
     for score, css, _clients in chains[:args.chains]:
         print(f"score: {rust_f64(score.value())}", file=out)
         sorted_config: List = []
@@ -84,6 +90,7 @@ def best_chains(args, out=sys.stdout) -> None:
             print(Search.stats_fmt(cs.stats, len(cs.config)), file=out)
         if args.show_order:  # (main.rs builds `sorted_config` but does not print it)
             print(f"sorted_config: {sorted_config!r}", file=out)
+    return 0
 
 
 def config_stats(args, out=sys.stdout) -> None:
@@ -220,7 +227,7 @@ def main(argv: Optional[Sequence[str]] = None, out=sys.stdout) -> int:
     if cmd == "main":
         if args.distance_table:
             print(distance_table(_planet(args), REGIONS13), file=out)
-        best_chains(args, out)
+        return best_chains(args, out)
     elif cmd == "distance-table":
         print(distance_table(_planet(args), args.regions.split(",")), file=out)
     elif cmd == "stats":

@@ -783,19 +783,54 @@ hipError_t launch_merge_sel(const Rec* src, uint32_t n_lists, const Rec* alt, ui
 }
 
 // ------------------------------------------------- one-launch list merge --
-// The per-block top-K lists of a sweep launch are mostly padding: after the
-// seed (bote_capi.hip sample_seed) a block list holds only the records that
-// beat a bound on the launch's K-th key, ~0-2 per objective.  One workgroup
-// per objective gathers the lists' filled prefixes (records before the first
-// rec_max) into LDS and sorts them with the running K least; lists whose
-// records do not fit one pass (WIDE_CAP) are taken in further passes, so the
-// result is the K least of the union whatever the fill (deterministic: the
-// (key, rank) order is total).  Replaces the 4-level merge_kernel tree of a
-// sweep's 1,024+ lists (one launch instead of four).
+// One workgroup per objective merges a sweep's per-block top-K lists (sorted,
+// padded with rec_max) into the K least of their union.  The group kernel's
+// dump (bote_group.hip, FastArgs::kbound) writes each list only up to the
+// least K-th key of any block, which still leaves most of every list: the
+// blocks take statistically similar chunks, so the least of 512 per-block
+// K-th order statistics leaves ~70 of each block's 100 records below it
+// (round 4: ~36 k records per objective, 1.07 ms per step).  So the merge
+// first tightens the bound from the lists' heads (BOTE_MERGE_HEADS):
+//   t = a key with at least K head records at or below it,
+// where the head records (the first WIDE_HEAD of each list) are distinct
+// configs, so the union's K-th key is <= t.  With 512 lists and K = 100 the
+// K-th least head lies at about the 20th percentile of the block minima, and
+// the union holds ~K + K/8 records at or below it.  t is found by a radix
+// select with 10-bit digits over (key - least head) that stops as soon as the
+// chosen digit's bin holds at most WIDE_SLACK heads beyond the K-th (one or
+// two passes for mean keys), and t is that bin's upper edge.  Each list's
+// prefix at or below min(t, kbound) is counted, the counts are scanned, and
+// when the gathered records fit one pass (<= WIDE_RANK_MAX) each record's
+// output slot is its rank among them (a count over LDS; the (key, rank) order
+// is total, so ranks are distinct); larger fills (the overflow fallback's full
+// lists, heavy ties at t) take the windowed bitonic path: passes of <=
+// WIDE_SORT - K records sorted with the running K least.  The result is the K
+// least of the union whatever the fill (tests/test_merge_model.py restates the
+// procedure and bounds the gathered count).
+#ifndef BOTE_MERGE_HEADS
+#define BOTE_MERGE_HEADS 1  // tighten the bound from the lists' heads (0: round 4's kbound only)
+#endif
 constexpr int WIDE_BD = 1024, WIDE_SORT = 4096, WIDE_LISTS_PER_THREAD = 4, WIDE_HEAD = 4;
+constexpr int WIDE_BINS = 1024, WIDE_WAVES = WIDE_BD / 64, WIDE_SLACK = 32, WIDE_RANK_MAX = 1024;
+// A record with key == ~0 (a NaN COV key) has a real rank < C(R, n) < 2^64 - 1,
+// so only padding matches both fields.
 __device__ __forceinline__ bool is_rec_max(const Rec& r) { return r.key == ~0ull && r.rank == ~0ull; }
 static_assert(WIDE_MERGE_LISTS == (uint32_t)(WIDE_BD * WIDE_LISTS_PER_THREAD), "one thread per WIDE_LISTS_PER_THREAD lists");
-size_t merge_wide_smem() { return (size_t)WIDE_SORT * sizeof(Rec) + (WIDE_BD + 8) * sizeof(uint32_t); }
+static_assert(WIDE_BINS == WIDE_BD, "the digit histogram shares the scan array");
+size_t merge_wide_smem() {
+  return (size_t)WIDE_SORT * sizeof(Rec) + (WIDE_BD + 8) * sizeof(uint32_t) + 4 * WIDE_WAVES * sizeof(uint64_t);
+}
+
+// inclusive prefix sum over the wavefront
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+  const uint32_t lane = threadIdx.x & 63;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(v, d);
+    if (lane >= (uint32_t)d) v += y;
+  }
+  return v;
+}
 
 __global__ void __launch_bounds__(WIDE_BD) merge_wide_kernel(const Rec* src, uint32_t n_lists, uint64_t list_stride,
                                                              Rec* dst, const Rec* alt, uint32_t alt_lists,
@@ -808,19 +843,22 @@ __global__ void __launch_bounds__(WIDE_BD) merge_wide_kernel(const Rec* src, uin
   }
   extern __shared__ __align__(16) unsigned char wsm[];
   Rec* buf = (Rec*)wsm;
-  uint32_t* scan = (uint32_t*)(wsm + (size_t)WIDE_SORT * sizeof(Rec));
-  uint32_t* ctl = scan + WIDE_BD;  // [0] next window start, [1] records this pass
-  const uint32_t o = blockIdx.x, tid = threadIdx.x;
+  uint32_t* scan = (uint32_t*)(wsm + (size_t)WIDE_SORT * sizeof(Rec));  // also the digit histogram
+  uint32_t* ctl = scan + WIDE_BD;  // [0] next window start, [1] records this pass; [2..4] the digit pick
+  uint64_t* red = (uint64_t*)(ctl + 8);  // per wave: least and greatest head key, head count, list records
+  const uint32_t o = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const uint32_t KK = K < (uint32_t)KP ? K : (uint32_t)KP;
+  Rec* out = dst + o * KP;
+  if (KK == 0) {
+    for (uint32_t i = tid; i < (uint32_t)KP; i += WIDE_BD) out[i] = rec_max();
+    return;
+  }
   // records above the bound on the K-th key (the least K-th key of the
   // group blocks' full lists) cannot be among the K least of the union
-  const uint64_t bound = kbound && !use_alt ? kbound[o] : ~0ull;
-  auto keep = [&](const Rec& r) { return !is_rec_max(r) && r.key <= bound; };
-  // per list: the filled prefix length (a sorted list padded with rec_max);
+  uint64_t bound = kbound && !use_alt ? kbound[o] : ~0ull;
   // the first WIDE_HEAD records of all of a thread's lists load together
   constexpr int H = WIDE_HEAD;
   Rec head[WIDE_LISTS_PER_THREAD][H];
-  uint32_t cnt[WIDE_LISTS_PER_THREAD], off[WIDE_LISTS_PER_THREAD], mine = 0;
 #pragma unroll
   for (int j = 0; j < WIDE_LISTS_PER_THREAD; ++j) {
     const uint32_t l = tid * WIDE_LISTS_PER_THREAD + j;
@@ -828,6 +866,108 @@ __global__ void __launch_bounds__(WIDE_BD) merge_wide_kernel(const Rec* src, uin
 #pragma unroll
     for (int c = 0; c < H; ++c) head[j][c] = l < n_lists && (uint32_t)c < KK ? L[c] : rec_max();
   }
+#if BOTE_MERGE_HEADS
+  {
+    // ---- t: a key with at least KK head records at or below it
+    const uint64_t b0 = bound;
+    // (a list's records end at its terminator: what follows it in memory is
+    // stale, so only the kept prefix of the heads counts)
+    uint32_t hn[WIDE_LISTS_PER_THREAD];
+#pragma unroll
+    for (int j = 0; j < WIDE_LISTS_PER_THREAD; ++j) {
+      uint32_t c = 0;
+#pragma unroll
+      for (int i = 0; i < H; ++i) c += (uint32_t)(c == (uint32_t)i && !is_rec_max(head[j][i]) && head[j][i].key <= b0);
+      hn[j] = c;
+    }
+    uint64_t mn = ~0ull, mx = 0, nh = 0;
+#pragma unroll
+    for (int j = 0; j < WIDE_LISTS_PER_THREAD; ++j)
+#pragma unroll
+      for (int c = 0; c < H; ++c)
+        if ((uint32_t)c < hn[j]) {
+          mn = min(mn, head[j][c].key);
+          mx = max(mx, head[j][c].key);
+          ++nh;
+        }
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+      mn = min(mn, (uint64_t)__shfl_xor((long long)mn, d));
+      mx = max(mx, (uint64_t)__shfl_xor((long long)mx, d));
+      nh += (uint64_t)__shfl_xor((long long)nh, d);
+    }
+    if (lane == 0) {
+      red[wv] = mn;
+      red[WIDE_WAVES + wv] = mx;
+      red[2 * WIDE_WAVES + wv] = nh;
+    }
+    __syncthreads();
+    mn = ~0ull;
+    mx = 0;
+    nh = 0;
+#pragma unroll
+    for (int w = 0; w < WIDE_WAVES; ++w) {
+      mn = min(mn, red[w]);
+      mx = max(mx, red[WIDE_WAVES + w]);
+      nh += red[2 * WIDE_WAVES + w];
+    }
+    if (nh >= KK) {  // (block-uniform)
+      uint64_t t = mn;
+      if (mx != mn) {
+        const uint64_t range = mx - mn;
+        uint32_t s_hi = 64 - (uint32_t)__clzll(range);  // every (key - mn) < 2^s_hi
+        uint64_t prefix = 0, need = KK;
+        for (;;) {
+          const uint32_t s_lo = s_hi > 10 ? s_hi - 10 : 0, w = s_hi - s_lo;
+          scan[tid] = 0;
+          __syncthreads();
+#pragma unroll
+          for (int j = 0; j < WIDE_LISTS_PER_THREAD; ++j)
+#pragma unroll
+            for (int c = 0; c < H; ++c)
+              if ((uint32_t)c < hn[j]) {
+                const uint64_t v = head[j][c].key - mn;
+                if (s_hi >= 64 || (v >> s_hi) == prefix)
+                  atomicAdd(&scan[(uint32_t)(v >> s_lo) & ((1u << w) - 1)], 1u);
+              }
+          __syncthreads();
+          if (wv == 0) {  // one wave: the bin holding the need-th head, 16 bins per lane
+            uint32_t cb[WIDE_BINS / 64], sl = 0;
+#pragma unroll
+            for (int q = 0; q < WIDE_BINS / 64; ++q) {
+              cb[q] = scan[lane * (WIDE_BINS / 64) + q];
+              sl += cb[q];
+            }
+            uint32_t before = wave_incl_scan(sl) - sl;
+#pragma unroll
+            for (int q = 0; q < WIDE_BINS / 64; ++q) {
+              if (before < need && need <= before + cb[q]) {  // exactly one lane, one bin
+                ctl[2] = lane * (WIDE_BINS / 64) + q;
+                ctl[3] = (uint32_t)(need - before);
+                ctl[4] = cb[q];
+              }
+              before += cb[q];
+            }
+          }
+          __syncthreads();
+          const uint32_t d = ctl[2], left = ctl[3], inbin = ctl[4];
+          prefix = (prefix << w) | d;
+          need = left;
+          s_hi = s_lo;
+          if (s_hi == 0 || inbin - left <= (uint32_t)WIDE_SLACK) break;  // (block-uniform)
+          __syncthreads();  // (ctl and the histogram are rewritten by the next pass)
+        }
+        const uint64_t x = (prefix << s_hi) | ((1ull << s_hi) - 1);  // (s_hi < 64 after a pass)
+        t = x > ~0ull - mn ? ~0ull : mn + x;
+      }
+      bound = min(bound, t);
+    }
+    __syncthreads();  // (the scan array is reused below)
+  }
+#endif
+  auto keep = [&](const Rec& r) { return !is_rec_max(r) && r.key <= bound; };
+  // per list: the filled prefix length at or below the bound
+  uint32_t cnt[WIDE_LISTS_PER_THREAD], off[WIDE_LISTS_PER_THREAD], mine = 0;
 #pragma unroll
   for (int j = 0; j < WIDE_LISTS_PER_THREAD; ++j) {
     uint32_t c = 0;
@@ -841,19 +981,42 @@ __global__ void __launch_bounds__(WIDE_BD) merge_wide_kernel(const Rec* src, uin
     off[j] = mine;
     mine += c;
   }
-  // exclusive scan of the threads' totals (list order = thread order)
-  scan[tid] = mine;
+  // exclusive scan of the threads' totals (list order = thread order): per
+  // wave by shuffles, then the waves' totals
+  const uint32_t incl = wave_incl_scan(mine);
+  if (lane == 63) scan[wv] = incl;
   __syncthreads();
-  for (uint32_t d = 1; d < WIDE_BD; d <<= 1) {
-    const uint32_t v = tid >= d ? scan[tid - d] : 0u;
-    __syncthreads();
-    scan[tid] += v;
-    __syncthreads();
+  uint32_t base = incl - mine, total = 0;
+#pragma unroll
+  for (uint32_t w = 0; w < (uint32_t)WIDE_WAVES; ++w) {
+    const uint32_t x = scan[w];
+    base += w < wv ? x : 0u;
+    total += x;
   }
-  const uint32_t base = scan[tid] - mine;  // records before this thread's lists
 #pragma unroll
   for (int j = 0; j < WIDE_LISTS_PER_THREAD; ++j) off[j] += base;
-  const uint32_t total = scan[WIDE_BD - 1];
+  if (total <= (uint32_t)WIDE_RANK_MAX) {  // (block-uniform) one pass: slot = rank among the gathered
+#pragma unroll
+    for (int j = 0; j < WIDE_LISTS_PER_THREAD; ++j) {
+      Rec* d = buf + off[j];
+#pragma unroll
+      for (int c = 0; c < H; ++c)
+        if ((uint32_t)c < cnt[j]) d[c] = head[j][c];
+      if (cnt[j] > (uint32_t)H) {
+        const Rec* L = src + (size_t)(tid * WIDE_LISTS_PER_THREAD + j) * list_stride + o * KP;
+        for (uint32_t c = H; c < cnt[j]; ++c) d[c] = L[c];
+      }
+    }
+    __syncthreads();
+    for (uint32_t i = tid; i < total; i += WIDE_BD) {
+      const Rec x = buf[i];
+      uint32_t r = 0;
+      for (uint32_t m = 0; m < total; ++m) r += (uint32_t)rec_lt(buf[m], x);
+      if (r < KK) out[r] = x;
+    }
+    for (uint32_t i = min(total, KK) + tid; i < (uint32_t)KP; i += WIDE_BD) out[i] = rec_max();
+    return;
+  }
   // running K least: buf[0 .. have)
   uint32_t have = 0;
   const uint32_t room = WIDE_SORT - KK;  // records gathered per pass
@@ -895,7 +1058,6 @@ __global__ void __launch_bounds__(WIDE_BD) merge_wide_kernel(const Rec* src, uin
     w0 = next;
   }
   __syncthreads();
-  Rec* out = dst + o * KP;
   for (uint32_t i = tid; i < (uint32_t)KP; i += WIDE_BD) out[i] = i < have && i < KK ? buf[i] : rec_max();
 }
 

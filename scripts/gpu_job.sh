@@ -16,6 +16,7 @@
 #   profile  rocprofv3 kernel trace + stats, then the PMC passes of
 #            scripts/summarize_profile.py, of bench.py on each workload in
 #            PWLS (default WL), to gpurun_out/$TAG/<workload>/
+#   trace    rocprofv3 kernel trace + stats (no counters) of bench.py for each workload in TWLS
 #   pmc      extra PMC passes: PASSES="ctr ...;ctr ..." over bench.py BENCH_ARGS
 #   shards   kernel trace of scripts/shard_ablate.py (per-dispatch cost of shards)
 #   ablate   scripts/ablate.py masks ABL on the -DBOTE_ABLATION library (lib_abl)
@@ -88,6 +89,17 @@ step_profile() {
         > "$P/pmc$i.log" 2>&1 || fail "pmc$i $wl" $? "$P/pmc$i.log"
       echo "pmc$i $wl ok"
     done
+  done
+}
+
+step_trace() {  # kernel trace + stats only (no PMC), for each workload in TWLS
+  export TMPDIR=/tmp
+  local wl
+  for wl in ${TWLS:-r64n7}; do
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/trace_$wl" -o run -- \
+      python3 bench.py --steps "${TSTEPS:-5}" --warmup 1 --no-cpu-baseline --workload "$wl" ${BENCH_ARGS:-} \
+      > "$O/trace_$wl.log" 2>&1 || fail "trace $wl" $? "$O/trace_$wl.log"
+    echo "trace $wl: $(grep -o '"ms_per_step": [0-9.]*\|"kernel_ms_avg": [0-9.]*\|"step_overhead_ms": [0-9.]*' "$O/trace_$wl.log" | tr '\n' ' ')"
   done
 }
 

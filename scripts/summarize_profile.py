@@ -25,9 +25,24 @@ def main():
     wl = sys.argv[2] if len(sys.argv) > 2 else "r64n7_n1"
     src = os.path.join(ROOT, "gpurun_out", tag)
     out = []
+    # the profiled library (bench.py's config.lib_build in the runs' own lines):
+    # bench.py quotes pmc.json / traffic.json figures only for that build
+    build = None
+    for lg in ("trace.log", "pmc1.log"):
+        p = os.path.join(src, lg)
+        if os.path.exists(p):
+            for line in open(p, errors="replace"):
+                if line.startswith("{") and '"lib_build"' in line:
+                    try:
+                        build = json.loads(line)["config"]["lib_build"]
+                    except (ValueError, KeyError):
+                        pass
+        if build:
+            break
     stats = os.path.join(src, "trace", "run_kernel_stats.csv")
     rows = list(csv.DictReader(open(stats)))
     out.append(f"# rocprofv3 summary {tag} ({wl})\n")
+    out.append(f"library build (sha256 prefix of libbote_hip.so, bench.py lib_build): `{build}`\n")
     out.append("## Kernel trace (`rocprofv3 --kernel-trace --stats`)\n")
     out.append("| kernel | calls | avg ms | min ms | max ms | % |")
     out.append("|---|---|---|---|---|---|")
@@ -109,7 +124,7 @@ def main():
                            "lds_insts_per_config": per.get("SQ_INSTS_LDS", 0) / lanes,
                            "salu_insts_per_config": per.get("SQ_INSTS_SALU", 0) / lanes,
                            "clock_ghz": clk, "kernel_ns": kns, "valu_issue_util": util,
-                           "source": f"profiles/{tag.replace('/', '_')}_profile.md"}
+                           "source": f"profiles/{tag.replace('/', '_')}_profile.md", "build": build}
                 out.append(f"VALU wave-instructions per config: {pmc[wl]['valu_insts_per_config']:.1f} "
                            f"(LDS {pmc[wl]['lds_insts_per_config']:.1f}, SALU {pmc[wl]['salu_insts_per_config']:.1f}); "
                            f"VALU issue utilisation (SQ_INSTS_VALU x 2 cyc / (1024 SIMD x cycles) at "
@@ -124,7 +139,7 @@ def main():
     if traffic is not None:
         p = os.path.join(ROOT, "profiles", "traffic.json")
         d = json.load(open(p)) if os.path.exists(p) else {}
-        d[wl] = traffic
+        d[wl] = {"bytes": traffic, "build": build, "source": f"profiles/{tag.replace('/', '_')}_profile.md"}
         json.dump(d, open(p, "w"), indent=1, sort_keys=True)
     print("\n".join(out))
 

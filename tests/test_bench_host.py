@@ -50,3 +50,29 @@ def test_cpu_baseline_small_sample(monkeypatch, keys):
     assert f"{len(objs)} objectives" in cb["sample"]
     assert ("extended key set" in cb["sample"]) == bool(keys)
     assert "drawn uniformly" in cb["sample"]
+
+
+def test_profile_figures_only_for_the_profiled_build():
+    """the line's VALU issue utilisation and HBM traffic come from
+    profiles/pmc.json / traffic.json; they are quoted only when those were
+    measured on the library being benched (bench.lib_build)."""
+    pmc = {"valu_insts_per_config": 869.0, "clock_ghz": 2.35, "build": "aaaa", "source": "x"}
+    traffic = {"bytes": 7.5e7, "build": "aaaa"}
+    valu, tb, stale = bench.profile_figures(pmc, traffic, "aaaa", 621216192, 14.45)
+    assert valu["same_build"] and 0.4 < valu["util"] < 0.6
+    assert tb == 7.5e7 and stale == []
+    valu, tb, stale = bench.profile_figures(pmc, traffic, "bbbb", 621216192, 14.45)
+    assert valu["util"] is None and not valu["same_build"]
+    assert tb is None and len(stale) == 2
+    # a figure without a build (before round 5) is never quoted
+    valu, tb, stale = bench.profile_figures(dict(pmc, build=None), None, "bbbb", 1, 1.0)
+    assert valu["util"] is None and tb is None and len(stale) == 1
+
+
+def test_lib_build_is_the_loaded_library():
+    from fantoch_amd import _lib
+
+    if not os.path.exists(_lib.LIB_PATH):
+        pytest.skip("library not built")
+    b = bench.lib_build()
+    assert len(b) == 16 and int(b, 16) >= 0

@@ -101,3 +101,15 @@ def test_main_reproduces_the_reference_binary(tmp_path):
     assert len(stats) == 6
     assert stats[1] == g["stats_fmt_n5"]
     assert lines[i + 7] == "sorted_config: [" + ", ".join(g["sorted_config"]) + "]"
+
+
+@pytest.mark.gpu
+def test_main_without_a_chain_fails_like_the_reference(tmp_path, capsys):
+    """main.rs:66-69 `.next().unwrap()` panics when no evolving chain exists:
+    ranking parameters no config meets give a non-zero exit and an error on
+    stderr, not an empty success."""
+    out = io.StringIO()
+    rc = cli.main(["--no-save-search", "--no-distance-table", "--ranking", "100000,100000,0,15"], out=out)
+    assert rc == 101
+    assert out.getvalue() == ""
+    assert "no evolving config chain" in capsys.readouterr().err
