@@ -130,6 +130,7 @@ struct bote_sweep {
   // run only when the deferred queue overflowed; chosen on the device)
   DBuf top_alt, counters_alt;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  hipEvent_t last0 = nullptr, last1 = nullptr;  // the last launch's kernel events (ev0/ev1 or a timing slot)
   // per-launch kernel timing since the last bote_sweep_timing_reset
   std::vector<std::pair<hipEvent_t, hipEvent_t>> evpool;
   size_t ev_used = 0;
@@ -1100,11 +1101,16 @@ static int merge_chain(bote_sweep* s, uint32_t lists, hipStream_t st, const unsi
                        uint32_t alt_lists = 0, const unsigned long long* kbound = nullptr) {
   const uint64_t lstride = (uint64_t)s->n_obj * bote::KP;
   Rec* rec_out = s->result.as<Rec>();
-  if (s->n_obj && kbound && wide_merge(lists, alt_lists)) {
-    // one launch: the lists' filled prefixes gathered and sorted in LDS
-    HIP_TRY(bote::launch_merge_wide(s->top.as<Rec>(), lists, s->top_alt.as<Rec>(), sel ? alt_lists : 0, lstride, sel,
-                                    QUEUE_CAP, kbound, rec_out, s->n_obj, s->K, st));
-  } else if (s->n_obj) {
+  uint64_t* cdst = (uint64_t*)((char*)s->result.p + lstride * 16);
+  if (s->n_obj && kbound && sel && wide_merge(lists, alt_lists)) {
+    // one launch: the lists' filled prefixes gathered and ranked in LDS, and
+    // the counters picked by the same device choice
+    HIP_TRY(bote::launch_merge_wide(s->top.as<Rec>(), lists, s->top_alt.as<Rec>(), alt_lists, lstride, sel, QUEUE_CAP,
+                                    kbound, rec_out, s->n_obj, s->K, s->counters.as<unsigned long long>(),
+                                    s->counters_alt.as<unsigned long long>(), cdst, st));
+    return BOTE_OK;
+  }
+  if (s->n_obj) {
     const Rec* src = s->top.as<Rec>();
     Rec* bufs[2] = {s->tmp0.as<Rec>(), s->tmp1.as<Rec>()};
     int b = 0;
@@ -1125,7 +1131,6 @@ static int merge_chain(bote_sweep* s, uint32_t lists, hipStream_t st, const unsi
     }
     if (lists) HIP_TRY(bote::launch_merge(src, lists, lstride, rec_out, lstride, s->n_obj, st));
   }
-  uint64_t* cdst = (uint64_t*)((char*)s->result.p + lstride * 16);
   if (sel) {
     HIP_TRY(bote::launch_pick_counters(s->counters.as<unsigned long long>(), s->counters_alt.as<unsigned long long>(),
                                        sel, QUEUE_CAP, cdst, st));
@@ -1160,11 +1165,11 @@ static int launch_generic(bote_sweep* s, uint64_t rb, uint64_t re, hipStream_t s
   hipEvent_t *e0 = nullptr, *e1 = nullptr;
   int rc;
   if (timed && (rc = timing_slot(s, e0, e1))) return rc;
-  HIP_TRY(hipEventRecord(s->ev0, st));
-  if (e0) HIP_TRY(hipEventRecord(*e0, st));
+  s->last0 = e0 ? *e0 : s->ev0;
+  s->last1 = e1 ? *e1 : s->ev1;
+  HIP_TRY(hipEventRecord(s->last0, st));
   HIP_TRY(bote::launch_eval(a, s->n, false, s->grid, s->bd, s->shm, st));
-  if (e1) HIP_TRY(hipEventRecord(*e1, st));
-  HIP_TRY(hipEventRecord(s->ev1, st));
+  HIP_TRY(hipEventRecord(s->last1, st));
   return merge_chain(s, s->grid, st);
 }
 
@@ -1176,6 +1181,9 @@ static int launch_generic(bote_sweep* s, uint64_t rb, uint64_t re, hipStream_t s
 #ifndef BOTE_SEED_STEPS
 #define BOTE_SEED_STEPS 8  // sample steps per wave (r03v A/B: 8 vs 1, kernel -1.6 %, 1/8 shard -5 %)
 #endif
+#ifndef BOTE_SEED_RUN
+#define BOTE_SEED_RUN 1  // consecutive steps per sample chunk (one group precompute per chunk)
+#endif
 static int sample_seed(bote_sweep* s, bote::FastArgs& f, uint64_t rb, uint64_t re, hipStream_t st) {
   const uint32_t nwaves = s->fgrid * (s->fargs.gbd / 64);
   const uint32_t base = std::min<uint32_t>(4096, nwaves);
@@ -1183,9 +1191,10 @@ static int sample_seed(bote_sweep* s, bote::FastArgs& f, uint64_t rb, uint64_t r
   // range.  (Chunks of 8 consecutive steps, 4,096 of them, measured slower:
   // kernel 15.52 vs 15.35 ms, their K least minima are a looser bound, r03x.)
   const uint64_t fit = (re - rb) / (64 * 8);
-  const uint32_t nsamp = (uint32_t)std::min<uint64_t>({(uint64_t)base * BOTE_SEED_STEPS, std::max<uint64_t>(base, fit), 65536});
-  if (nsamp < s->K || re - rb < (uint64_t)nsamp * 64 * 8) return BOTE_OK;
-  const uint32_t ssteps = 1;
+  const uint32_t ssteps = BOTE_SEED_RUN;
+  const uint32_t nsamp = (uint32_t)std::min<uint64_t>(
+      {(uint64_t)base * std::max(1, BOTE_SEED_STEPS / BOTE_SEED_RUN), std::max<uint64_t>(base, fit / ssteps), 65536});
+  if (nsamp < s->K || re - rb < (uint64_t)nsamp * ssteps * 64 * 8) return BOTE_OK;
   auto key = std::make_pair(rb, re);
   auto it = s->samples.find(key);
   if (it == s->samples.end()) {
@@ -1289,12 +1298,13 @@ static int launch_fast_path(bote_sweep* s, uint64_t rb, uint64_t re, hipStream_t
   hipEvent_t *e0 = nullptr, *e1 = nullptr;
   int rc;
   if ((rc = timing_slot(s, e0, e1))) return rc;
-  HIP_TRY(hipEventRecord(s->ev0, st));
-  HIP_TRY(hipEventRecord(*e0, st));
-  if (s->group) HIP_TRY(bote::launch_group(f, s->n, s->def_obj, s->fgrid, s->fshm, st));
-  else HIP_TRY(bote::launch_fast(f, s->n, s->fgrid, s->fshm, st));
-  HIP_TRY(hipEventRecord(*e1, st));
-  HIP_TRY(hipEventRecord(s->ev1, st));
+  // the kernel's events ride on its dispatch (hipExtLaunchKernelGGL): a
+  // separate hipEventRecord before and after the kernel left ~10 us of idle
+  // GPU each (profiles/r05b trace)
+  s->last0 = *e0;
+  s->last1 = *e1;
+  if (s->group) HIP_TRY(bote::launch_group(f, s->n, s->def_obj, s->fgrid, s->fshm, st, *e0, *e1));
+  else HIP_TRY(bote::launch_fast(f, s->n, s->fgrid, s->fshm, st, *e0, *e1));
   // exact fixup of the deferred configs: generic kernel over the rank list
   EvalArgs a = s->args;
   a.rank_list = s->queue.as<uint64_t>();
@@ -1406,8 +1416,8 @@ int bote_merge_device(const bote_sweep* s, const void* src, uint32_t n_shards, v
 int bote_sweep_last_kernel_ms(bote_sweep* s, float* out_ms) {
   if (!s || !out_ms) return fail(BOTE_E_ARG, "null argument");
   if (!s->launched) return fail(BOTE_E_ARG, "sweep not launched");
-  HIP_TRY(hipEventSynchronize(s->ev1));
-  HIP_TRY(hipEventElapsedTime(out_ms, s->ev0, s->ev1));
+  HIP_TRY(hipEventSynchronize(s->last1));
+  HIP_TRY(hipEventElapsedTime(out_ms, s->last0, s->last1));
   return BOTE_OK;
 }
 

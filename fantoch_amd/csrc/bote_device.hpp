@@ -2,6 +2,7 @@
 // search.  Integer min/select work on VALU; no MFMA (DESIGN.md "Roofline").
 #pragma once
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <stdint.h>
 
 namespace bote {

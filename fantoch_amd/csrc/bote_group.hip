@@ -374,6 +374,19 @@ __device__ __forceinline__ float u64_to_f32(uint64_t x) {
 #ifndef BOTE_GROUP_UNROLL
 #define BOTE_GROUP_UNROLL 4
 #endif
+// BIN client loop: both clients' member tags of a packed word are masked in
+// one v_and (fast class), then each bin address is one v_mad_u32_u16 of a
+// half (op_sel picks the high one) instead of v_and / v_bfe + v_lshl_add
+// (profiles/r05e issue rates: v_mad_u32_u16 0.91, v_and 1.62, v_bfe and
+// v_lshl_add 0.95 wave-instructions per CU-clock)
+#ifndef BOTE_BIN_MAD16
+#define BOTE_BIN_MAD16 1
+#endif
+// BIN client loop: a loop without the in-loop flush test when one 32-bit sum
+// of squared keys holds every client (k_flush >= the quads)
+#ifndef BOTE_BIN_NOFLUSH
+#define BOTE_BIN_NOFLUSH 1
+#endif
 // BN: the base key set with the member-binned client loop (the extended key
 // set's, below); the host picks it for bench-shaped sweeps with >= 96 clients
 // (FastArgs::gbins: R=128 n=6 179.8 -> 168.2 ms; neutral at 64 clients)
@@ -1291,6 +1304,15 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
                   asm("v_lshl_add_u32 %0, %1, 8, %2" : "=v"(r) : "v"(t), "v"(bin));
                   return r;
                 };
+                // both bin addresses of a packed pair of keys: the tags masked
+                // together (t = w & 0x000F000F), then bin + 256 t.lo16 and
+                // bin + 256 t.hi16 by v_mad_u32_u16 (op_sel selects the half)
+                const uint32_t k256 = 256u;
+                auto baddr2 = [&](uint32_t w, uint32_t& lo, uint32_t& hi) {
+                  const uint32_t t = w & 0x000F000Fu;
+                  asm("v_mad_u32_u16 %0, %1, %2, %3" : "=v"(lo) : "v"(t), "v"(k256), "v"(bin));
+                  asm("v_mad_u32_u16 %0, %1, %2, %3 op_sel:[1,0,0,0]" : "=v"(hi) : "v"(t), "v"(k256), "v"(bin));
+                };
                 // (the keys of a group of quads are read before any of their
                 // bin adds: the compiler cannot tell the bins from the CQT and
                 // lines, so it keeps program order between LDS reads and adds)
@@ -1313,6 +1335,16 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
                   // L2 follows from their sum and the bins (below)
                   s2l = __builtin_amdgcn_udot2(as_us2(L), as_us2(L), s2l, false);
                   s2l = __builtin_amdgcn_udot2(as_us2(H), as_us2(H), s2l, false);
+                  if (BOTE_BIN_MAD16 && nv >= 4) {
+                    uint32_t aL0, aL1, aH0, aH1;
+                    baddr2(L, aL0, aL1);
+                    baddr2(H, aH0, aH1);
+                    badd(aL0, __builtin_amdgcn_perm(0x01000000u, L, 0x070C0100u));
+                    badd(aL1, __builtin_amdgcn_perm(0x01000000u, L, 0x070C0302u));
+                    badd(aH0, __builtin_amdgcn_perm(0x01000000u, H, 0x070C0100u));
+                    badd(aH1, __builtin_amdgcn_perm(0x01000000u, H, 0x070C0302u));
+                    return;
+                  }
                   badd(baddr(L & 15u), __builtin_amdgcn_perm(0x01000000u, L, 0x070C0100u));
                   if (nv >= 2) badd(baddr(__builtin_amdgcn_ubfe(L, 16, 4)), __builtin_amdgcn_perm(0x01000000u, L, 0x070C0302u));
                   if (nv >= 3) badd(baddr(H & 15u), __builtin_amdgcn_perm(0x01000000u, H, 0x070C0100u));
@@ -1325,7 +1357,24 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
                   constexpr uint32_t UB = decltype(lines_c)::value ? 4u : 2u;
                   const uint32_t fU = a.k_flush / UB ? a.k_flush / UB : 1u;
                   uint32_t g = 0, k = 0;
-                  if (a.k_flush >= UB) {
+                  if (BOTE_BIN_NOFLUSH && a.k_flush >= nql + UB) {
+                    // one 32-bit sum holds every client's squared key: no
+                    // flush test in the loop (a uniform branch)
+                    for (; g + UB <= nql; g += UB) {
+                      uint32_t Lk[UB], Hk[UB];
+#pragma unroll
+                      for (uint32_t u = 0; u < UB; u += 2) {
+                        us2 lo0, hi0, lo1, hi1;
+                        nearest2(lines_c, g * 8 + 8 * u, lo0, hi0, lo1, hi1);
+                        Lk[u] = as_u32(lo0);
+                        Hk[u] = as_u32(hi0);
+                        Lk[u + 1] = as_u32(lo1);
+                        Hk[u + 1] = as_u32(hi1);
+                      }
+#pragma unroll
+                      for (uint32_t u = 0; u < UB; ++u) quad_bin(Lk[u], Hk[u], 4u);
+                    }
+                  } else if (a.k_flush >= UB) {
                     for (; g + UB <= nql; g += UB) {
                       uint32_t Lk[UB], Hk[UB];
 #pragma unroll
@@ -1768,11 +1817,15 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
 
 // ------------------------------------------------------------- launcher ---
 template <int N, bool DEF, bool SI, bool RXC, bool XK, bool BN = false>
-static hipError_t launch_group_n(const FastArgs& a, uint32_t grid, size_t shm, hipStream_t st) {
+static hipError_t launch_group_n(const FastArgs& a, uint32_t grid, size_t shm, hipStream_t st, hipEvent_t e0,
+                                 hipEvent_t e1) {
   auto k = sweep_group_kernel<N, DEF, SI, RXC, XK, BN>;
   hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k, dim3(grid), dim3(a.gbd), shm, st, a);
+  // (timed launches carry their events in the dispatch: no marker packets
+  // before and after the kernel, which cost ~10 us of idle GPU each)
+  if (e0) hipExtLaunchKernelGGL(k, dim3(grid), dim3(a.gbd), (uint32_t)shm, st, e0, e1, 0u, a);
+  else hipLaunchKernelGGL(k, dim3(grid), dim3(a.gbd), shm, st, a);
   return hipGetLastError();
 }
 
@@ -1801,19 +1854,20 @@ static const void* group_fn_n(const FastArgs& a, bool def) {
 }
 
 template <int N, bool XK>
-static hipError_t launch_group_x(const FastArgs& a, bool def, uint32_t grid, size_t shm, hipStream_t st) {
+static hipError_t launch_group_x(const FastArgs& a, bool def, uint32_t grid, size_t shm, hipStream_t st, hipEvent_t e0,
+                                 hipEvent_t e1) {
   if constexpr (XK) {
-    return group_si(a) ? (a.grx ? launch_group_n<N, true, true, true, true>(a, grid, shm, st)
-                                : launch_group_n<N, true, true, false, true>(a, grid, shm, st))
-                       : launch_group_n<N, true, false, false, true>(a, grid, shm, st);
+    return group_si(a) ? (a.grx ? launch_group_n<N, true, true, true, true>(a, grid, shm, st, e0, e1)
+                                : launch_group_n<N, true, true, false, true>(a, grid, shm, st, e0, e1))
+                       : launch_group_n<N, true, false, false, true>(a, grid, shm, st, e0, e1);
   } else {
     if (def && group_si(a) && a.gbins)
-      return a.grx ? launch_group_n<N, true, true, true, false, true>(a, grid, shm, st)
-                   : launch_group_n<N, true, true, false, false, true>(a, grid, shm, st);
-    return def ? (group_si(a) ? (a.grx ? launch_group_n<N, true, true, true, false>(a, grid, shm, st)
-                                       : launch_group_n<N, true, true, false, false>(a, grid, shm, st))
-                              : launch_group_n<N, true, false, false, false>(a, grid, shm, st))
-               : launch_group_n<N, false, false, false, false>(a, grid, shm, st);
+      return a.grx ? launch_group_n<N, true, true, true, false, true>(a, grid, shm, st, e0, e1)
+                   : launch_group_n<N, true, true, false, false, true>(a, grid, shm, st, e0, e1);
+    return def ? (group_si(a) ? (a.grx ? launch_group_n<N, true, true, true, false>(a, grid, shm, st, e0, e1)
+                                       : launch_group_n<N, true, true, false, false>(a, grid, shm, st, e0, e1))
+                              : launch_group_n<N, true, false, false, false>(a, grid, shm, st, e0, e1))
+               : launch_group_n<N, false, false, false, false>(a, grid, shm, st, e0, e1);
   }
 }
 
@@ -1844,12 +1898,13 @@ int group_occupancy(const FastArgs& a, uint32_t n, size_t shm, bool def) {
   return nb > 0 ? nb : 0;
 }
 
-hipError_t launch_group(const FastArgs& a, uint32_t n, bool def, uint32_t grid, size_t shm, hipStream_t st) {
+hipError_t launch_group(const FastArgs& a, uint32_t n, bool def, uint32_t grid, size_t shm, hipStream_t st, hipEvent_t e0,
+                        hipEvent_t e1) {
   switch (n) {
 #define GS_CASE(NN) \
-  case NN: return a.keys ? launch_group_x<NN, true>(a, def, grid, shm, st) : launch_group_x<NN, false>(a, def, grid, shm, st);
+  case NN: return a.keys ? launch_group_x<NN, true>(a, def, grid, shm, st, e0, e1) : launch_group_x<NN, false>(a, def, grid, shm, st, e0, e1);
 #define GS_CASE0(NN) \
-  case NN: return a.keys ? hipErrorInvalidValue : launch_group_x<NN, false>(a, def, grid, shm, st);
+  case NN: return a.keys ? hipErrorInvalidValue : launch_group_x<NN, false>(a, def, grid, shm, st, e0, e1);
 #ifdef BOTE_ISA_N7  // (analysis builds only: the n = 7 kernels, for assembly listings)
     GS_CASE(7)
 #elif defined(BOTE_ISA_N6)  // (the n = 6 kernels: BASELINE config 5)

@@ -810,7 +810,7 @@ hipError_t launch_merge_sel(const Rec* src, uint32_t n_lists, const Rec* alt, ui
 #ifndef BOTE_MERGE_HEADS
 #define BOTE_MERGE_HEADS 1  // tighten the bound from the lists' heads (0: round 4's kbound only)
 #endif
-constexpr int WIDE_BD = 1024, WIDE_SORT = 4096, WIDE_LISTS_PER_THREAD = 4, WIDE_HEAD = 4;
+constexpr int WIDE_BD = 1024, WIDE_SORT = 4096, WIDE_LISTS_PER_THREAD = 4, WIDE_HEAD = 2;
 constexpr int WIDE_BINS = 1024, WIDE_WAVES = WIDE_BD / 64, WIDE_SLACK = 32, WIDE_RANK_MAX = 1024;
 // A record with key == ~0 (a NaN COV key) has a real rank < C(R, n) < 2^64 - 1,
 // so only padding matches both fields.
@@ -832,20 +832,124 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
   return v;
 }
 
+// Block-wide selection for merge_wide_kernel: among the values the threads
+// visit (each(f) calls f(v) for each of this thread's values), a value x with
+// at least `need` values <= x, by an MSB-first radix select with 10-bit digits
+// over (v - least value) that stops as soon as the chosen digit's bin holds at
+// most WIDE_SLACK values beyond the need-th, or at the exact value.  `left` is
+// then the need-th value's position among the values of the final bin and
+// `inbin` their number (exact: x is the need-th value itself).  none: fewer
+// than `need` values.  Every thread of the block calls it (it has barriers).
+struct WideSel {
+  uint64_t x;
+  uint32_t left, inbin;
+  bool exact, none;
+};
+template <class Each>
+__device__ WideSel wide_select(Each each, uint64_t need, uint32_t* hist, uint32_t* ctl, uint64_t* red, bool slack) {
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  uint64_t mn = ~0ull, mx = 0, nv = 0;
+  each([&](uint64_t v) {
+    mn = min(mn, v);
+    mx = max(mx, v);
+    ++nv;
+  });
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {
+    mn = min(mn, (uint64_t)__shfl_xor((long long)mn, d));
+    mx = max(mx, (uint64_t)__shfl_xor((long long)mx, d));
+    nv += (uint64_t)__shfl_xor((long long)nv, d);
+  }
+  if (lane == 0) {
+    red[wv] = mn;
+    red[WIDE_WAVES + wv] = mx;
+    red[2 * WIDE_WAVES + wv] = nv;
+  }
+  __syncthreads();
+  mn = ~0ull;
+  mx = 0;
+  nv = 0;
+#pragma unroll
+  for (int w = 0; w < WIDE_WAVES; ++w) {
+    mn = min(mn, red[w]);
+    mx = max(mx, red[WIDE_WAVES + w]);
+    nv += red[2 * WIDE_WAVES + w];
+  }
+  WideSel r{~0ull, 0, 0, false, true};
+  if (nv >= need && need > 0) {  // (block-uniform)
+    r.none = false;
+    if (mx == mn) {
+      r = WideSel{mn, (uint32_t)need, (uint32_t)nv, true, false};
+    } else {
+      uint32_t s_hi = 64 - (uint32_t)__clzll(mx - mn);  // every (v - mn) < 2^s_hi
+      uint64_t prefix = 0;
+      for (;;) {
+        const uint32_t s_lo = s_hi > 10 ? s_hi - 10 : 0, w = s_hi - s_lo;
+        hist[tid] = 0;
+        __syncthreads();
+        each([&](uint64_t v) {
+          v -= mn;
+          if (s_hi >= 64 || (v >> s_hi) == prefix) atomicAdd(&hist[(uint32_t)(v >> s_lo) & ((1u << w) - 1)], 1u);
+        });
+        __syncthreads();
+        if (wv == 0) {  // one wave: the bin holding the need-th value, 16 bins per lane
+          uint32_t cb[WIDE_BINS / 64], sl = 0;
+#pragma unroll
+          for (int q = 0; q < WIDE_BINS / 64; ++q) {
+            cb[q] = hist[lane * (WIDE_BINS / 64) + q];
+            sl += cb[q];
+          }
+          uint32_t before = wave_incl_scan(sl) - sl;
+#pragma unroll
+          for (int q = 0; q < WIDE_BINS / 64; ++q) {
+            if (before < need && need <= before + cb[q]) {  // exactly one lane, one bin
+              ctl[2] = lane * (WIDE_BINS / 64) + q;
+              ctl[3] = (uint32_t)(need - before);
+              ctl[4] = cb[q];
+            }
+            before += cb[q];
+          }
+        }
+        __syncthreads();
+        const uint32_t d = ctl[2], left = ctl[3], inbin = ctl[4];
+        prefix = (prefix << w) | d;
+        need = left;
+        s_hi = s_lo;
+        if (s_hi == 0 || (slack && inbin - left <= (uint32_t)WIDE_SLACK)) {  // (block-uniform)
+          r.left = left;
+          r.inbin = inbin;
+          r.exact = s_hi == 0;
+          break;
+        }
+        __syncthreads();  // (the histogram and ctl are rewritten by the next pass)
+      }
+      const uint64_t x = (prefix << s_hi) | ((1ull << s_hi) - 1);  // (s_hi < 64 after a pass)
+      r.x = x > ~0ull - mn ? ~0ull : mn + x;
+    }
+  }
+  __syncthreads();  // (red, hist and ctl are reused by the caller)
+  return r;
+}
+
 __global__ void __launch_bounds__(WIDE_BD) merge_wide_kernel(const Rec* src, uint32_t n_lists, uint64_t list_stride,
                                                              Rec* dst, const Rec* alt, uint32_t alt_lists,
                                                              const unsigned long long* sel, uint64_t cap,
-                                                             const unsigned long long* kbound, uint32_t K) {
+                                                             const unsigned long long* kbound, uint32_t K,
+                                                             const unsigned long long* csrc,
+                                                             const unsigned long long* calt, uint64_t* cdst) {
   const bool use_alt = sel && *sel > cap;
   if (use_alt) {  // device-side choice of the input (fast sweep overflow fallback)
     src = alt;
     n_lists = alt_lists;
   }
+  // the result's counters (valid, digest) from the same choice (what
+  // pick_counters_kernel does for the merge tree; one launch fewer)
+  if (cdst && blockIdx.x == 0 && threadIdx.x < 2) cdst[threadIdx.x] = (use_alt ? calt : csrc)[threadIdx.x];
   extern __shared__ __align__(16) unsigned char wsm[];
   Rec* buf = (Rec*)wsm;
   uint32_t* scan = (uint32_t*)(wsm + (size_t)WIDE_SORT * sizeof(Rec));  // also the digit histogram
   uint32_t* ctl = scan + WIDE_BD;  // [0] next window start, [1] records this pass; [2..4] the digit pick
-  uint64_t* red = (uint64_t*)(ctl + 8);  // per wave: least and greatest head key, head count, list records
+  uint64_t* red = (uint64_t*)(ctl + 8);  // per wave: least and greatest value, count
   const uint32_t o = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const uint32_t KK = K < (uint32_t)KP ? K : (uint32_t)KP;
   Rec* out = dst + o * KP;
@@ -853,128 +957,97 @@ __global__ void __launch_bounds__(WIDE_BD) merge_wide_kernel(const Rec* src, uin
     for (uint32_t i = tid; i < (uint32_t)KP; i += WIDE_BD) out[i] = rec_max();
     return;
   }
+  constexpr int LT = WIDE_LISTS_PER_THREAD, H = WIDE_HEAD;
+  auto list = [&](int j) { return src + (size_t)(tid * LT + j) * list_stride + o * KP; };
+  auto live = [&](int j) { return tid * LT + (uint32_t)j < n_lists; };
   // records above the bound on the K-th key (the least K-th key of the
   // group blocks' full lists) cannot be among the K least of the union
-  uint64_t bound = kbound && !use_alt ? kbound[o] : ~0ull;
-  // the first WIDE_HEAD records of all of a thread's lists load together
-  constexpr int H = WIDE_HEAD;
-  Rec head[WIDE_LISTS_PER_THREAD][H];
+  const uint64_t b0 = kbound && !use_alt ? kbound[o] : ~0ull;
+  // the keys of the first WIDE_HEAD records of all of a thread's lists load
+  // together into LDS (the gather buffer, free until the gather; in
+  // registers they spilled at 1,024 threads), thread-minor: conflict-free
+  static_assert(WIDE_LISTS_PER_THREAD * WIDE_HEAD * 8 <= 16 * WIDE_SORT / WIDE_BD, "head keys fit the gather buffer");
+  uint64_t* hkl = (uint64_t*)buf;
+  auto hk = [&](int j, int c) -> uint64_t& { return hkl[(c * LT + j) * WIDE_BD + tid]; };
 #pragma unroll
-  for (int j = 0; j < WIDE_LISTS_PER_THREAD; ++j) {
-    const uint32_t l = tid * WIDE_LISTS_PER_THREAD + j;
-    const Rec* L = src + (size_t)l * list_stride + o * KP;
+  for (int j = 0; j < LT; ++j)
 #pragma unroll
-    for (int c = 0; c < H; ++c) head[j][c] = l < n_lists && (uint32_t)c < KK ? L[c] : rec_max();
-  }
+    for (int c = 0; c < H; ++c) hk(j, c) = live(j) && (uint32_t)c < KK ? list(j)[c].key : ~0ull;
+  // the bound record (bk, br): the union's K least are at or below it
+  uint64_t bk = ~0ull, br = ~0ull;
 #if BOTE_MERGE_HEADS
   {
-    // ---- t: a key with at least KK head records at or below it
-    const uint64_t b0 = bound;
-    // (a list's records end at its terminator: what follows it in memory is
-    // stale, so only the kept prefix of the heads counts)
-    uint32_t hn[WIDE_LISTS_PER_THREAD];
+    // the heads' kept prefix per list (a list's records end at its
+    // terminator: what follows it in memory is stale; a key of all ones, a
+    // NaN COV, also ends it here: fewer heads only loosen the bound)
+    uint32_t hn[LT];
 #pragma unroll
-    for (int j = 0; j < WIDE_LISTS_PER_THREAD; ++j) {
+    for (int j = 0; j < LT; ++j) {
       uint32_t c = 0;
 #pragma unroll
-      for (int i = 0; i < H; ++i) c += (uint32_t)(c == (uint32_t)i && !is_rec_max(head[j][i]) && head[j][i].key <= b0);
+      for (int i = 0; i < H; ++i) c += (uint32_t)(c == (uint32_t)i && hk(j, i) != ~0ull && hk(j, i) <= b0);
       hn[j] = c;
     }
-    uint64_t mn = ~0ull, mx = 0, nh = 0;
+    auto each_head = [&](auto f) {
 #pragma unroll
-    for (int j = 0; j < WIDE_LISTS_PER_THREAD; ++j)
+      for (int j = 0; j < LT; ++j)
 #pragma unroll
-      for (int c = 0; c < H; ++c)
-        if ((uint32_t)c < hn[j]) {
-          mn = min(mn, head[j][c].key);
-          mx = max(mx, head[j][c].key);
-          ++nh;
-        }
+        for (int c = 0; c < H; ++c)
+          if ((uint32_t)c < hn[j]) f(hk(j, c));
+    };
+    // (to the exact key: a bin's worth of heads above the K-th could stand
+    // for many more tied records beyond the heads)
+    const WideSel ks = wide_select(each_head, KK, scan, ctl, red, false);
+    if (!ks.none) {
+      bk = ks.x;
+      if (ks.inbin > 1) {
+        // heads tie at the K-th key (FPaxos means: round 5 measured 1,186
+        // records at one key on a 1/8 shard): the left-th least rank among
+        // them makes (bk, br) the K-th least head record itself
+        auto each_tie = [&](auto f) {
 #pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) {
-      mn = min(mn, (uint64_t)__shfl_xor((long long)mn, d));
-      mx = max(mx, (uint64_t)__shfl_xor((long long)mx, d));
-      nh += (uint64_t)__shfl_xor((long long)nh, d);
-    }
-    if (lane == 0) {
-      red[wv] = mn;
-      red[WIDE_WAVES + wv] = mx;
-      red[2 * WIDE_WAVES + wv] = nh;
-    }
-    __syncthreads();
-    mn = ~0ull;
-    mx = 0;
-    nh = 0;
-#pragma unroll
-    for (int w = 0; w < WIDE_WAVES; ++w) {
-      mn = min(mn, red[w]);
-      mx = max(mx, red[WIDE_WAVES + w]);
-      nh += red[2 * WIDE_WAVES + w];
-    }
-    if (nh >= KK) {  // (block-uniform)
-      uint64_t t = mn;
-      if (mx != mn) {
-        const uint64_t range = mx - mn;
-        uint32_t s_hi = 64 - (uint32_t)__clzll(range);  // every (key - mn) < 2^s_hi
-        uint64_t prefix = 0, need = KK;
-        for (;;) {
-          const uint32_t s_lo = s_hi > 10 ? s_hi - 10 : 0, w = s_hi - s_lo;
-          scan[tid] = 0;
-          __syncthreads();
-#pragma unroll
-          for (int j = 0; j < WIDE_LISTS_PER_THREAD; ++j)
+          for (int j = 0; j < LT; ++j)
 #pragma unroll
             for (int c = 0; c < H; ++c)
-              if ((uint32_t)c < hn[j]) {
-                const uint64_t v = head[j][c].key - mn;
-                if (s_hi >= 64 || (v >> s_hi) == prefix)
-                  atomicAdd(&scan[(uint32_t)(v >> s_lo) & ((1u << w) - 1)], 1u);
-              }
-          __syncthreads();
-          if (wv == 0) {  // one wave: the bin holding the need-th head, 16 bins per lane
-            uint32_t cb[WIDE_BINS / 64], sl = 0;
-#pragma unroll
-            for (int q = 0; q < WIDE_BINS / 64; ++q) {
-              cb[q] = scan[lane * (WIDE_BINS / 64) + q];
-              sl += cb[q];
-            }
-            uint32_t before = wave_incl_scan(sl) - sl;
-#pragma unroll
-            for (int q = 0; q < WIDE_BINS / 64; ++q) {
-              if (before < need && need <= before + cb[q]) {  // exactly one lane, one bin
-                ctl[2] = lane * (WIDE_BINS / 64) + q;
-                ctl[3] = (uint32_t)(need - before);
-                ctl[4] = cb[q];
-              }
-              before += cb[q];
-            }
-          }
-          __syncthreads();
-          const uint32_t d = ctl[2], left = ctl[3], inbin = ctl[4];
-          prefix = (prefix << w) | d;
-          need = left;
-          s_hi = s_lo;
-          if (s_hi == 0 || inbin - left <= (uint32_t)WIDE_SLACK) break;  // (block-uniform)
-          __syncthreads();  // (ctl and the histogram are rewritten by the next pass)
-        }
-        const uint64_t x = (prefix << s_hi) | ((1ull << s_hi) - 1);  // (s_hi < 64 after a pass)
-        t = x > ~0ull - mn ? ~0ull : mn + x;
+              if ((uint32_t)c < hn[j] && hk(j, c) == bk) f(list(j)[c].rank);
+        };
+        const WideSel rs = wide_select(each_tie, ks.left, scan, ctl, red, true);
+        if (!rs.none) br = rs.x;
       }
-      bound = min(bound, t);
     }
-    __syncthreads();  // (the scan array is reused below)
+#ifdef BOTE_MERGE_PRINTF
+    if (tid == 0)
+      printf("merge o=%u lists=%u b0=%llx bk=%llx br=%llx exact=%d inbin=%u left=%u\n", o, n_lists,
+             (unsigned long long)b0, (unsigned long long)bk, (unsigned long long)br, (int)ks.exact, ks.inbin, ks.left);
+#endif
   }
 #endif
-  auto keep = [&](const Rec& r) { return !is_rec_max(r) && r.key <= bound; };
-  // per list: the filled prefix length at or below the bound
-  uint32_t cnt[WIDE_LISTS_PER_THREAD], off[WIDE_LISTS_PER_THREAD], mine = 0;
+  const uint64_t kb = min(b0, bk);
+  // a record is gathered when it is a real record at or below both bounds
+  auto keep = [&](const Rec& r) {
+    return !is_rec_max(r) && r.key <= kb && (r.key < bk || r.rank <= br);
+  };
+  // per list: the filled prefix length at or below the bound (keys from the
+  // registers; a rank is read only where it decides)
+  uint32_t cnt[LT], off[LT], mine = 0;
 #pragma unroll
-  for (int j = 0; j < WIDE_LISTS_PER_THREAD; ++j) {
+  for (int j = 0; j < LT; ++j) {
     uint32_t c = 0;
+    bool go = live(j);
 #pragma unroll
-    for (int i = 0; i < H; ++i) c += (uint32_t)(c == (uint32_t)i && keep(head[j][i]));
-    if (c == (uint32_t)H) {  // a long list (rare): walk the rest
-      const Rec* L = src + (size_t)(tid * WIDE_LISTS_PER_THREAD + j) * list_stride + o * KP;
+    for (int i = 0; i < H; ++i) {
+      if (go && (uint32_t)i < KK) {
+        const uint64_t k = hk(j, i);
+        bool in = k <= kb;
+        if (in && (k == ~0ull || (k == bk && br != ~0ull))) in = keep(list(j)[i]);
+        c += in ? 1u : 0u;
+        go = in;
+      } else {
+        go = false;
+      }
+    }
+    if (go) {  // a long list (rare): walk the rest
+      const Rec* L = list(j);
       while (c < KK && keep(L[c])) ++c;
     }
     cnt[j] = c;
@@ -982,7 +1055,8 @@ __global__ void __launch_bounds__(WIDE_BD) merge_wide_kernel(const Rec* src, uin
     mine += c;
   }
   // exclusive scan of the threads' totals (list order = thread order): per
-  // wave by shuffles, then the waves' totals
+  // wave by shuffles, then the waves' totals (the barrier also ends the head
+  // keys' use of the gather buffer)
   const uint32_t incl = wave_incl_scan(mine);
   if (lane == 63) scan[wv] = incl;
   __syncthreads();
@@ -994,18 +1068,15 @@ __global__ void __launch_bounds__(WIDE_BD) merge_wide_kernel(const Rec* src, uin
     total += x;
   }
 #pragma unroll
-  for (int j = 0; j < WIDE_LISTS_PER_THREAD; ++j) off[j] += base;
+  for (int j = 0; j < LT; ++j) off[j] += base;
+#ifdef BOTE_MERGE_PRINTF
+  if (tid == 0) printf("merge o=%u total=%u\n", o, total);
+#endif
   if (total <= (uint32_t)WIDE_RANK_MAX) {  // (block-uniform) one pass: slot = rank among the gathered
 #pragma unroll
-    for (int j = 0; j < WIDE_LISTS_PER_THREAD; ++j) {
-      Rec* d = buf + off[j];
-#pragma unroll
-      for (int c = 0; c < H; ++c)
-        if ((uint32_t)c < cnt[j]) d[c] = head[j][c];
-      if (cnt[j] > (uint32_t)H) {
-        const Rec* L = src + (size_t)(tid * WIDE_LISTS_PER_THREAD + j) * list_stride + o * KP;
-        for (uint32_t c = H; c < cnt[j]; ++c) d[c] = L[c];
-      }
+    for (int j = 0; j < LT; ++j) {
+      const Rec* L = list(j);
+      for (uint32_t c = 0; c < cnt[j]; ++c) buf[off[j] + c] = L[c];
     }
     __syncthreads();
     for (uint32_t i = tid; i < total; i += WIDE_BD) {
@@ -1030,16 +1101,12 @@ __global__ void __launch_bounds__(WIDE_BD) merge_wide_kernel(const Rec* src, uin
     __syncthreads();
     // lists inside [w0, w0 + room) are copied after the running list
 #pragma unroll
-    for (int j = 0; j < WIDE_LISTS_PER_THREAD; ++j) {
-      const uint32_t l = tid * WIDE_LISTS_PER_THREAD + j;
+    for (int j = 0; j < LT; ++j) {
       if (cnt[j] == 0 || off[j] < w0) continue;
       if (off[j] + cnt[j] - w0 <= room) {
         Rec* d = buf + KK + off[j] - w0;
-#pragma unroll
-        for (int c = 0; c < H; ++c)
-          if ((uint32_t)c < cnt[j]) d[c] = head[j][c];
-        const Rec* L = src + (size_t)l * list_stride + o * KP;
-        for (uint32_t c = H; c < cnt[j]; ++c) d[c] = L[c];
+        const Rec* L = list(j);
+        for (uint32_t c = 0; c < cnt[j]; ++c) d[c] = L[c];
         atomicMax(&ctl[1], off[j] + cnt[j] - w0);
       } else {
         atomicMin(&ctl[0], off[j]);
@@ -1063,7 +1130,8 @@ __global__ void __launch_bounds__(WIDE_BD) merge_wide_kernel(const Rec* src, uin
 
 hipError_t launch_merge_wide(const Rec* src, uint32_t n_lists, const Rec* alt, uint32_t alt_lists, uint64_t list_stride,
                              const unsigned long long* sel, uint64_t cap, const unsigned long long* kbound, Rec* dst,
-                             uint32_t n_obj, uint32_t K, hipStream_t st) {
+                             uint32_t n_obj, uint32_t K, const unsigned long long* csrc, const unsigned long long* calt,
+                             uint64_t* cdst, hipStream_t st) {
   if (n_lists > (uint32_t)(WIDE_BD * WIDE_LISTS_PER_THREAD) || alt_lists > (uint32_t)(WIDE_BD * WIDE_LISTS_PER_THREAD))
     return hipErrorInvalidValue;
   const size_t shm = merge_wide_smem();
@@ -1079,7 +1147,7 @@ hipError_t launch_merge_wide(const Rec* src, uint32_t n_lists, const Rec* alt, u
     done.fetch_or(bit, std::memory_order_relaxed);
   }
   hipLaunchKernelGGL(merge_wide_kernel, dim3(n_obj), dim3(WIDE_BD), shm, st, src, n_lists, list_stride, dst, alt,
-                     alt_lists, sel, cap, kbound, K);
+                     alt_lists, sel, cap, kbound, K, csrc, calt, cdst);
   return hipGetLastError();
 }
 

@@ -210,7 +210,9 @@ struct FastArgs {
 #endif
 size_t fast_smem_bytes(const FastArgs& a, uint32_t n);
 int fast_occupancy(uint32_t n, size_t shm);
-hipError_t launch_fast(const FastArgs& a, uint32_t n, uint32_t grid, size_t shm, hipStream_t st);
+// (e0, e1: events carried by the dispatch itself, hipExtLaunchKernelGGL, for a timed launch)
+hipError_t launch_fast(const FastArgs& a, uint32_t n, uint32_t grid, size_t shm, hipStream_t st, hipEvent_t e0 = nullptr,
+                       hipEvent_t e1 = nullptr);
 size_t group_smem_bytes(const FastArgs& a, uint32_t n);
 bool group_uses_lines(uint32_t n);  // n <= 7: client lines (FastArgs::gslots) and register lookups
 // the extended key set's group kernels are bounded to this workgroup size (3
@@ -226,7 +228,8 @@ bool group_supports_keys(uint32_t n, uint32_t bd);  // the extended key set on t
 // workgroups per CU of the kernel instantiation launch_group runs for `a`
 // (workgroup size a.gbd)
 int group_occupancy(const FastArgs& a, uint32_t n, size_t shm, bool def_objectives);
-hipError_t launch_group(const FastArgs& a, uint32_t n, bool def_objectives, uint32_t grid, size_t shm, hipStream_t st);
+hipError_t launch_group(const FastArgs& a, uint32_t n, bool def_objectives, uint32_t grid, size_t shm, hipStream_t st,
+                        hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);
 
 size_t eval_smem_bytes(const EvalArgs& a, uint32_t n, uint32_t bd, bool topk);
 int eval_occupancy(uint32_t n, bool full, uint32_t bd, size_t shm, bool keys = false);
@@ -239,9 +242,12 @@ hipError_t launch_merge(const Rec* src, uint32_t n_lists, uint64_t list_stride, 
 constexpr uint32_t WIDE_MERGE_LISTS = 4096;
 // one launch for a sweep's block lists (<= WIDE_MERGE_LISTS lists): the K least per
 // objective into dst[o * KP] (sel/alt/cap: the overflow fallback's choice)
+// csrc/calt/cdst: the counters (valid, digest) copied to cdst by the same
+// device choice (sel) as the lists, as launch_pick_counters does
 hipError_t launch_merge_wide(const Rec* src, uint32_t n_lists, const Rec* alt, uint32_t alt_lists, uint64_t list_stride,
                              const unsigned long long* sel, uint64_t cap, const unsigned long long* kbound, Rec* dst,
-                             uint32_t n_obj, uint32_t K, hipStream_t st);
+                             uint32_t n_obj, uint32_t K, const unsigned long long* csrc, const unsigned long long* calt,
+                             uint64_t* cdst, hipStream_t st);
 hipError_t launch_merge_sel(const Rec* src, uint32_t n_lists, const Rec* alt, uint32_t alt_lists, uint64_t list_stride,
                             const unsigned long long* sel, uint64_t cap, Rec* dst, uint64_t out_stride, uint32_t n_obj,
                             hipStream_t st);

@@ -463,11 +463,13 @@ __global__ void __launch_bounds__(FAST_BD, 4) sweep_fast_kernel(FastArgs a) {
 
 // ------------------------------------------------------------- launcher ---
 template <int N>
-static hipError_t launch_fast_n(const FastArgs& a, uint32_t grid, size_t shm, hipStream_t st) {
+static hipError_t launch_fast_n(const FastArgs& a, uint32_t grid, size_t shm, hipStream_t st, hipEvent_t e0,
+                                hipEvent_t e1) {
   auto k = sweep_fast_kernel<N>;
   hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k, dim3(grid), dim3(FAST_BD), shm, st, a);
+  if (e0) hipExtLaunchKernelGGL(k, dim3(grid), dim3(FAST_BD), (uint32_t)shm, st, e0, e1, 0u, a);
+  else hipLaunchKernelGGL(k, dim3(grid), dim3(FAST_BD), shm, st, a);
   return hipGetLastError();
 }
 
@@ -486,9 +488,10 @@ int fast_occupancy(uint32_t n, size_t shm) {
   return nb > 0 ? nb : 1;
 }
 
-hipError_t launch_fast(const FastArgs& a, uint32_t n, uint32_t grid, size_t shm, hipStream_t st) {
+hipError_t launch_fast(const FastArgs& a, uint32_t n, uint32_t grid, size_t shm, hipStream_t st, hipEvent_t e0,
+                       hipEvent_t e1) {
   switch (n) {
-#define FS_CASE(NN) case NN: return launch_fast_n<NN>(a, grid, shm, st);
+#define FS_CASE(NN) case NN: return launch_fast_n<NN>(a, grid, shm, st, e0, e1);
     FS_CASE(2) FS_CASE(3) FS_CASE(4) FS_CASE(5) FS_CASE(6) FS_CASE(7) FS_CASE(8) FS_CASE(9)
     FS_CASE(10) FS_CASE(11) FS_CASE(12) FS_CASE(13) FS_CASE(14) FS_CASE(15) FS_CASE(16)
 #undef FS_CASE

@@ -54,6 +54,60 @@ KERNEL(k_mul_f32, "v_mul_f32_e32 %0, %0, %1")
 KERNEL(k_fma_f32, "v_fma_f32 %0, %0, %1, %1")
 KERNEL(k_rcp_f32, "v_rcp_f32_e32 %0, %0")
 KERNEL(k_cndmask, "v_cndmask_b32_e32 %0, %0, %1, vcc")
+// round 5: candidates for the binned client loop's tag/address/value ops
+KERNEL(k_add_sdwa_w1, "v_add_u32_sdwa %0, %0, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:DWORD")
+KERNEL(k_add_sdwa_w0, "v_add_u32_sdwa %0, %0, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_0 src1_sel:DWORD")
+KERNEL(k_mad_u16_hi, "v_mad_u32_u16 %0, %0, %1, %1 op_sel:[1,0,0,0]")
+KERNEL(k_mad_u16, "v_mad_u32_u16 %0, %0, %1, %1")
+KERNEL(k_and_const, "v_and_b32_e32 %0, 0xf000f, %0")
+// v_cndmask_b32_e32 measured 0.175: which part is slow (the VCC read, any
+// SGPR-pair mask, an SGPR operand)?
+#define KERNEL_S(NAME, INS)                                                                              \
+  __global__ void __launch_bounds__(256) NAME(unsigned* out, unsigned iters, unsigned seed) {           \
+    unsigned a0 = threadIdx.x ^ seed, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4, a5 = a0 + 5, \
+             a6 = a0 + 6, a7 = a0 + 7, k = seed * 3u + 1u;                                              \
+    unsigned long long m = __ballot(threadIdx.x & 1);                                                   \
+    unsigned sk = __builtin_amdgcn_readfirstlane(seed * 5u);                                            \
+    for (unsigned i = 0; i < iters; ++i) {                                                               \
+      C8S(INS) C8S(INS) C8S(INS) C8S(INS)                                                                \
+    }                                                                                                    \
+    unsigned s = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;                                                 \
+    if (s == 0x12345678u) out[blockIdx.x] = s;                                                           \
+  }
+#define C8S(INS)                                                                                         \
+  asm volatile(INS : "+v"(a0) : "v"(k), "s"(m), "s"(sk)); asm volatile(INS : "+v"(a1) : "v"(k), "s"(m), "s"(sk)); \
+  asm volatile(INS : "+v"(a2) : "v"(k), "s"(m), "s"(sk)); asm volatile(INS : "+v"(a3) : "v"(k), "s"(m), "s"(sk)); \
+  asm volatile(INS : "+v"(a4) : "v"(k), "s"(m), "s"(sk)); asm volatile(INS : "+v"(a5) : "v"(k), "s"(m), "s"(sk)); \
+  asm volatile(INS : "+v"(a6) : "v"(k), "s"(m), "s"(sk)); asm volatile(INS : "+v"(a7) : "v"(k), "s"(m), "s"(sk));
+KERNEL_S(k_cnd_sgpr, "v_cndmask_b32_e64 %0, %0, %1, %2")
+KERNEL_S(k_add_sgpr, "v_add_u32_e32 %0, %3, %0")
+KERNEL_S(k_min_sgpr, "v_min_u32_e32 %0, %3, %0")
+KERNEL_S(k_cnd_vcc_set, "s_mov_b64 vcc, %2\n v_cndmask_b32_e32 %0, %0, %1, vcc")
+// mixes: 7 v_add + 1 mask select per 8 instructions
+#define C8M(INS, SEL)                                                                                    \
+  asm volatile(INS : "+v"(a0) : "v"(k), "s"(m), "s"(sk)); asm volatile(INS : "+v"(a1) : "v"(k), "s"(m), "s"(sk)); \
+  asm volatile(INS : "+v"(a2) : "v"(k), "s"(m), "s"(sk)); asm volatile(INS : "+v"(a3) : "v"(k), "s"(m), "s"(sk)); \
+  asm volatile(INS : "+v"(a4) : "v"(k), "s"(m), "s"(sk)); asm volatile(INS : "+v"(a5) : "v"(k), "s"(m), "s"(sk)); \
+  asm volatile(INS : "+v"(a6) : "v"(k), "s"(m), "s"(sk)); asm volatile(SEL : "+v"(a7) : "v"(k), "s"(m), "s"(sk));
+#define KERNEL_M(NAME, INS, SEL)                                                                         \
+  __global__ void __launch_bounds__(256) NAME(unsigned* out, unsigned iters, unsigned seed) {           \
+    unsigned a0 = threadIdx.x ^ seed, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4, a5 = a0 + 5, \
+             a6 = a0 + 6, a7 = a0 + 7, k = seed * 3u + 1u;                                              \
+    unsigned long long m = __ballot(threadIdx.x & 1);                                                   \
+    unsigned sk = __builtin_amdgcn_readfirstlane(seed * 5u);                                            \
+    for (unsigned i = 0; i < iters; ++i) {                                                               \
+      C8M(INS, SEL) C8M(INS, SEL) C8M(INS, SEL) C8M(INS, SEL)                                            \
+    }                                                                                                    \
+    unsigned s = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;                                                 \
+    if (s == 0x12345678u) out[blockIdx.x] = s;                                                           \
+  }
+KERNEL_M(k_mix_add8, "v_add_u32_e32 %0, %0, %1", "v_add_u32_e32 %0, %0, %1")
+KERNEL_M(k_mix_cndvcc, "v_add_u32_e32 %0, %0, %1", "v_cndmask_b32_e32 %0, %0, %1, vcc")
+KERNEL_M(k_mix_cnds, "v_add_u32_e32 %0, %0, %1", "v_cndmask_b32_e64 %0, %0, %1, %2")
+KERNEL_M(k_mix_addc, "v_add_u32_e32 %0, %0, %1", "v_addc_co_u32_e32 %0, vcc, %0, %1, vcc")
+KERNEL_M(k_mix_sgpr, "v_add_u32_e32 %0, %0, %1", "v_add_u32_e32 %0, %3, %0")
+KERNEL(k_add_co, "v_add_co_u32_e32 %0, vcc, %0, %1")
+KERNEL(k_lshr_sdwa, "v_lshrrev_b32_sdwa %0, %1, %0 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1")
 
 typedef void (*kfn)(unsigned*, unsigned, unsigned);
 
@@ -69,7 +123,15 @@ int main() {
       {"v_and_or_b32", k_and_or, 8},   {"v_lshl_or_b32", k_lshl_or, 8}, {"v_alignbit_b32", k_alignbit, 8},
       {"v_mul_lo_u32", k_mul_lo, 8},   {"v_cvt_f32_u32", k_cvt_f32, 4}, {"v_mul_f32", k_mul_f32, 4},
       {"v_fma_f32", k_fma_f32, 8},     {"v_rcp_f32", k_rcp_f32, 4},
-      {"v_cndmask_b32", k_cndmask, 4}};
+      {"v_cndmask_b32", k_cndmask, 4},
+      {"v_add_u32_sdwa WORD_1", k_add_sdwa_w1, 8}, {"v_add_u32_sdwa WORD_0", k_add_sdwa_w0, 8},
+      {"v_mad_u32_u16 op_sel hi", k_mad_u16_hi, 8}, {"v_mad_u32_u16", k_mad_u16, 8},
+      {"v_and_b32 literal", k_and_const, 8},  {"v_lshrrev_b32_sdwa", k_lshr_sdwa, 8},
+      {"v_cndmask_b32_e64 sgpr mask", k_cnd_sgpr, 8}, {"v_add_u32 sgpr operand", k_add_sgpr, 4},
+      {"v_min_u32 sgpr operand", k_min_sgpr, 4}, {"s_mov vcc + v_cndmask (per op)", k_cnd_vcc_set, 8},
+      {"mix 8 v_add", k_mix_add8, 4}, {"mix 7 v_add + 1 v_cndmask vcc", k_mix_cndvcc, 4},
+      {"mix 7 v_add + 1 v_cndmask s-mask", k_mix_cnds, 4}, {"mix 7 v_add + 1 v_addc vcc", k_mix_addc, 4},
+      {"mix 7 v_add + 1 v_add sgpr", k_mix_sgpr, 4}, {"v_add_co_u32 (writes vcc)", k_add_co, 4}};
   hipDeviceProp_t prop;
   hipGetDeviceProperties(&prop, 0);
   const unsigned cus = prop.multiProcessorCount, threads = 256, iters = 2048;

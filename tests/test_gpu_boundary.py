@@ -273,3 +273,44 @@ def test_sweep_split_bounds():
     got = merge_gathered(sw, gathered, 8)
     assert (got.valid, got.digest) == (fx["valid"], fx["digest"])
     assert got.tops == [[tuple(r) for r in t] for t in fx["tops"]]
+
+
+def test_step_overhead_outside_the_sweep_kernel():
+    """Guard rail (the per-step cost outside the sweep kernel grew
+    4.5x unnoticed): back-to-back full R=64 n=7 sweeps on one stream, each
+    with its result copied to pinned host memory, as bench.py's steps are.
+    Wall time per step minus the event-timed kernel (the HIP events ride on
+    the kernel's dispatch) -- the zeroing, sample launch, seed, fix-up, merge
+    and copy -- stays below 0.3 ms (round 5: ~0.2 ms of a 14.6 ms step)."""
+    import time
+
+    import torch
+
+    p = Planet.synthetic(64)
+    dp = DevicePlanet(p)
+    srv = np.arange(64, dtype=np.uint32)
+    sw = Sweep(dp, srv, srv, 7, DEFAULT_OBJECTIVES, K=100, ranking=DEFAULT_RANKING, digest=True)
+    stream = torch.cuda.current_stream().cuda_stream
+    host = torch.empty(sw.result_bytes(), dtype=torch.uint8, pin_memory=True)
+    for _ in range(2):
+        sw.launch(0, sw.total, stream)
+        sw.result_device(host.data_ptr(), stream)
+    torch.cuda.synchronize()
+    sw.timing_reset()
+    steps = 8
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        sw.launch(0, sw.total, stream)
+        sw.result_device(host.data_ptr(), stream)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / steps * 1e3
+    kms, n = sw.timing()
+    over = dt - kms / n
+    print(f"step {dt:.3f} ms, sweep kernel {kms / n:.3f} ms, outside the kernel {over:.3f} ms")
+    assert n == steps
+    assert over < 0.3
+    fx = os.path.join(GOLDEN, "syn_r64n7_full.json")
+    if os.path.exists(fx):
+        f = json.load(open(fx))
+        r = sw.parse_block(host.numpy())
+        assert (r.valid, str(r.digest)) == (f["valid"], str(f["digest"]))

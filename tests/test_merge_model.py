@@ -57,33 +57,28 @@ def dump(lists, K, order):
     return out, bound
 
 
-WIDE_HEAD, WIDE_SLACK, WIDE_RANK_MAX = 4, 32, 1024
+WIDE_HEAD, WIDE_SLACK, WIDE_RANK_MAX = 2, 32, 1024
+ONES = 2**64 - 1
 
 
-def head_bound(dumped, K, b0, H=WIDE_HEAD, slack=WIDE_SLACK):
-    """merge_wide_kernel's heads' bound: a key with at least K kept head
-    records at or below it (all-ones: none).  The kept heads of a list are the
-    prefix of its first min(H, K) records before the first record that is
-    padding or above b0 (the memory after a terminator is stale)."""
-    heads = []
-    for L in dumped:
-        for r in L[:min(H, K)]:
-            if r == REC_MAX or r[0] > b0:
-                break
-            heads.append(r[0])
-    if len(heads) < K:
-        return 2**64 - 1
-    mn, mx = min(heads), max(heads)
+def wide_select(values, need, slack=WIDE_SLACK, stop_early=True):
+    """merge_wide_kernel's wide_select: a value x with at least `need` values
+    <= x, by a radix select with 10-bit digits over (v - least) that stops
+    once the chosen bin holds at most `slack` values beyond the need-th, or at
+    the exact value.  Returns (x, left, inbin, exact) or None (too few)."""
+    if len(values) < need or need == 0:
+        return None
+    mn, mx = min(values), max(values)
     if mn == mx:
-        return mn
+        return mn, need, len(values), True
     s_hi = (mx - mn).bit_length()
-    prefix, need = 0, K
+    prefix = 0
     while True:
         s_lo = max(s_hi - 10, 0)
         w = s_hi - s_lo
         hist = [0] * 1024
-        for k in heads:
-            v = k - mn
+        for v in values:
+            v -= mn
             if s_hi >= 64 or (v >> s_hi) == prefix:
                 hist[(v >> s_lo) & ((1 << w) - 1)] += 1
         before = 0
@@ -95,33 +90,57 @@ def head_bound(dumped, K, b0, H=WIDE_HEAD, slack=WIDE_SLACK):
         prefix = (prefix << w) | d
         need = left
         s_hi = s_lo
-        if s_hi == 0 or inbin - left <= slack:
+        if s_hi == 0 or (stop_early and inbin - left <= slack):
             break
     x = (prefix << s_hi) | ((1 << s_hi) - 1)
-    return min(2**64 - 1, mn + x)
+    return min(ONES, mn + x), left, inbin, s_hi == 0
 
 
-def prefix_counts(dumped, K, bound):
+def head_bound(dumped, K, b0, H=WIDE_HEAD, slack=WIDE_SLACK):
+    """merge_wide_kernel's bound record (bk, br): the K-th least head key
+    (selected to the exact key), and when several heads tie at it, the
+    matching rank among the tied heads (a rank bound that may stop within
+    `slack` ranks), so (bk, br) is about the K-th least head record.  The heads are each list's kept prefix of its
+    first min(H, K) records: before the first record that is padding, has a
+    key of all ones or lies above b0 (the memory after a terminator is
+    stale)."""
+    heads = []
+    for L in dumped:
+        for r in L[:min(H, K)]:
+            if r == REC_MAX or r[0] == ONES or r[0] > b0:
+                break
+            heads.append(r)
+    ks = wide_select([k for k, _ in heads], K, slack, stop_early=False)
+    if ks is None:
+        return ONES, ONES
+    bk, left, inbin, exact = ks
+    br = ONES
+    if inbin > 1:
+        rs = wide_select([rk for k, rk in heads if k == bk], left, slack)
+        if rs is not None:
+            br = rs[0]
+    return bk, br
+
+
+def keep(r, b0, bk, br):
+    return r != REC_MAX and r[0] <= min(b0, bk) and (r[0] < bk or r[1] <= br)
+
+
+def prefix_counts(dumped, K, b0, bk=ONES, br=ONES):
     cnt = []
     for L in dumped:
         c = 0
-        while c < K and L[c] != REC_MAX and L[c][0] <= bound:
+        while c < K and keep(L[c], b0, bk, br):
             c += 1
         cnt.append(c)
     return cnt
 
 
 def wide_merge(dumped, K, bound, room, heads=True):
-    """merge_wide_kernel: the heads' bound, prefix counts, exclusive scan,
-    then one pass ranked by counting or windows of `room`."""
-    if heads:
-        bound = min(bound, head_bound(dumped, K, bound))
-    cnt = []
-    for L in dumped:
-        c = 0
-        while c < K and L[c] != REC_MAX and L[c][0] <= bound:
-            c += 1
-        cnt.append(c)
+    """merge_wide_kernel: the heads' bound record, prefix counts, exclusive
+    scan, then one pass ranked by counting or windows of `room`."""
+    bk, br = head_bound(dumped, K, bound) if heads else (ONES, ONES)
+    cnt = prefix_counts(dumped, K, bound, bk, br)
     off, acc = [], 0
     for c in cnt:
         off.append(acc)
@@ -178,8 +197,8 @@ def test_stale_records_after_a_terminator_are_not_heads():
     K = 4
     stale = [(0, 1000 + i) for i in range(8)]  # small keys: would pull the bound down
     dumped = [[(50, 0), REC_MAX] + stale, [(60, 1), REC_MAX] + stale, [(70, 2), (71, 3), (72, 4), (73, 5)]]
-    t = head_bound(dumped, K, 2**64 - 1)
-    assert t >= 71  # the 4th least real head
+    bk, br = head_bound(dumped, K, 2**64 - 1, H=4)
+    assert bk >= 71  # the 4th least real head
     got = wide_merge(dumped, K, 2**64 - 1, 4096 - K)
     assert got == [(50, 0), (60, 1), (70, 2), (71, 3)]
 
@@ -207,8 +226,8 @@ def test_gathered_records_stay_near_k(objective, blocks):
     random.Random(blocks).shuffle(order)
     dumped, kb = dump(lists, K, order)
     loose = sum(prefix_counts(dumped, K, kb))
-    t = min(kb, head_bound(dumped, K, kb))
-    tight = sum(prefix_counts(dumped, K, t))
+    bk, br = head_bound(dumped, K, kb)
+    tight = sum(prefix_counts(dumped, K, kb, bk, br))
     assert tight >= K
     assert tight <= 2 * K, (tight, loose)
     assert tight <= WIDE_RANK_MAX
@@ -251,3 +270,30 @@ def test_per_wave_sample_minima_bound_the_kth_key(seed):
     every = sorted(k for ch in chunks for k in ch)
     if len(every) >= K and seed_key != 2**64 - 1:
         assert every[K - 1] <= seed_key
+
+
+@pytest.mark.parametrize("blocks", [64, 544, 4096])
+def test_heavy_ties_at_the_kth_key_are_bounded_by_rank(blocks):
+    """FPaxos mean keys tie heavily (round 5, R=64 n=7 1/8 shard: over 100
+    heads share the least key, and the key bound alone gathered 1,186
+    records, past the one-pass limit).  The tied heads' rank bound keeps the
+    gathered records near K."""
+    rng = np.random.default_rng(7 + blocks)
+    K, per_block = 100, 2000
+    # ticket chunks spread every block over the whole rank space: the blocks'
+    # ranks interleave (distinct across blocks)
+    ranks = rng.permutation(blocks * per_block).reshape(blocks, per_block)
+    lists = []
+    for b in range(blocks):
+        # a few distinct small keys, each shared by many configs of the block
+        keys = rng.choice([1000, 1000, 1000, 1001, 1003, 1010], size=per_block)
+        lists.append(sorted((int(k), int(r)) for k, r in zip(keys, ranks[b]))[:K])
+    dumped, kb = dump(lists, K, list(range(blocks)))
+    bk, br = head_bound(dumped, K, kb)
+    keys_only = sum(prefix_counts(dumped, K, kb, bk, ONES))
+    tight = sum(prefix_counts(dumped, K, kb, bk, br))
+    assert K <= tight <= 2 * K + 64, (tight, keys_only)
+    if blocks >= 544:
+        assert keys_only > WIDE_RANK_MAX  # the key bound alone: every list's ties
+    got = wide_merge(dumped, K, kb, 4096 - K)
+    assert got == sorted(r for L in lists for r in L)[:K]
