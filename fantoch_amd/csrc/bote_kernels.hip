@@ -817,8 +817,10 @@ constexpr int WIDE_BINS = 1024, WIDE_WAVES = WIDE_BD / 64, WIDE_SLACK = 32, WIDE
 __device__ __forceinline__ bool is_rec_max(const Rec& r) { return r.key == ~0ull && r.rank == ~0ull; }
 static_assert(WIDE_MERGE_LISTS == (uint32_t)(WIDE_BD * WIDE_LISTS_PER_THREAD), "one thread per WIDE_LISTS_PER_THREAD lists");
 static_assert(WIDE_BINS == WIDE_BD, "the digit histogram shares the scan array");
+constexpr int WIDE_FEW = 64;  // a bin this small is finished by one wave (wide_select)
 size_t merge_wide_smem() {
-  return (size_t)WIDE_SORT * sizeof(Rec) + (WIDE_BD + 8) * sizeof(uint32_t) + 4 * WIDE_WAVES * sizeof(uint64_t);
+  return (size_t)WIDE_SORT * sizeof(Rec) + (WIDE_BD + 8) * sizeof(uint32_t) + 4 * WIDE_WAVES * sizeof(uint64_t) +
+         WIDE_FEW * sizeof(uint64_t);
 }
 
 // inclusive prefix sum over the wavefront
@@ -848,6 +850,7 @@ struct WideSel {
 template <class Each>
 __device__ WideSel wide_select(Each each, uint64_t need, uint32_t* hist, uint32_t* ctl, uint64_t* red, bool slack) {
   const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  uint64_t* few = red + 4 * WIDE_WAVES;  // the values of a small final bin
   uint64_t mn = ~0ull, mx = 0, nv = 0;
   each([&](uint64_t v) {
     mn = min(mn, v);
@@ -909,6 +912,7 @@ __device__ WideSel wide_select(Each each, uint64_t need, uint32_t* hist, uint32_
             }
             before += cb[q];
           }
+          if (lane == 0) ctl[5] = 0;  // (slots of a small bin's values)
         }
         __syncthreads();
         const uint32_t d = ctl[2], left = ctl[3], inbin = ctl[4];
@@ -920,6 +924,36 @@ __device__ WideSel wide_select(Each each, uint64_t need, uint32_t* hist, uint32_
           r.inbin = inbin;
           r.exact = s_hi == 0;
           break;
+        }
+        if (inbin <= (uint32_t)WIDE_FEW) {  // (block-uniform) the bin's values to one wave: exact
+          each([&](uint64_t v) {
+            v -= mn;
+            if ((v >> s_hi) == prefix) few[atomicAdd(&ctl[5], 1u)] = v;
+          });
+          __syncthreads();
+          if (wv == 0) {
+            // the left-th least: the value with fewer than `left` values below it
+            // and at least `left` at or below it (ties: every lane holding it agrees)
+            const uint64_t x = lane < inbin ? few[lane] : ~0ull;
+            uint32_t lt = 0, le = 0;
+            for (uint32_t j = 0; j < inbin; ++j) {
+              const uint64_t y = few[j];
+              lt += (uint32_t)(y < x);
+              le += (uint32_t)(y <= x);
+            }
+            if (lane < inbin && lt < left && left <= le) {
+              red[0] = x;
+              ctl[3] = left - lt;  // (its position among the values equal to it)
+              ctl[4] = le - lt;
+            }
+          }
+          __syncthreads();
+          r.x = mn + red[0];
+          r.left = ctl[3];
+          r.inbin = ctl[4];
+          r.exact = true;
+          __syncthreads();
+          return r;
         }
         __syncthreads();  // (the histogram and ctl are rewritten by the next pass)
       }

@@ -27,6 +27,7 @@ Issue cost: fast class ~1.6 wave-instr per CU-clock, slow ~0.95
 (profiles/r02_issue_rate_ops.json), so a slow op costs ~1.7 fast ones.
 """
 import json
+import os
 import sys
 from collections import Counter, defaultdict
 
@@ -34,15 +35,61 @@ sys.path.insert(0, __file__.rsplit("/", 1)[0])
 from isa_lines import DEFAULT_SECTIONS, parse  # noqa: E402
 from isa_mix import classify  # noqa: E402
 
-RARE_MARK = ("_f64", "v_div_", "global_atomic", "ds_cmpst", "ds_cmpswap", "s_sleep", "s_ff1", "v_rcp_f64",
-             "v_sqrt_f64")
+RARE_MARK = ("v_div_", "global_atomic", "ds_cmpst", "ds_cmpswap", "s_sleep", "s_ff1", "v_rcp_f64", "v_sqrt_f64")
+# f64 ARITHMETIC marks a rare path (the exact decisions inside the f64
+# ambiguity bands); f64 <-> f32 conversions do not: every step converts the
+# leader column's V (vcol) to f32 for the screens, and round 4's model, which
+# zeroed every block with any f64 op, missed ~135 VALU per step in the leader
+# choice block that holds that conversion
+import re  # noqa: E402
+RARE_F64 = re.compile(r"^v_(add|mul|fma|mad|ldexp|max|min|cmp[a-z_]*|frexp[a-z_]*|fract|trunc|floor)_f64")
+
+
+def is_rare_op(o):
+    return any(m in o for m in RARE_MARK) or bool(RARE_F64.match(o))
 FAST_RATE, SLOW_RATE = 1.6, 0.95
+
+
+# Rare regions: the body of an `if` that runs for a whole wavefront only when
+# some lane takes it, weighted by its measured frequency per wave-step
+# (scripts/pathstats.py, the -DBOTE_PATHSTATS build).  A region is the source
+# lines from the marker line to its matching closing brace (the marker is the
+# `if` line that follows the PSTAT site); a block is charged to the innermost
+# region that holds most of its bote_group.hip lines.
+RARE_REGIONS = [
+    ("if (amb) {  // exact re-scan", "leader re-scan"),
+    ("mok = (mom_mean(mf) - mom_mean(ma)) >= a.p_fmean;", "f64 mean test f=1"),
+    ("if (defer) {", "validity deferred"),
+    ("PSTAT(a, 9, maybe);", "f64 score"),
+    ("PSTAT(a, 10, maybe);", "COV af1 key"),
+]
+
+
+def region_lines(src, marker):
+    """(first, last) 1-based lines of the region a marker opens: a marker line
+    with an opening brace runs to its matching brace; a PSTAT line, to the
+    end of the `if` block on the next line; any other line is itself."""
+    i = next(k for k, l in enumerate(src) if marker in l)
+    if marker.startswith("PSTAT"):
+        i += 1
+    if "{" not in src[i]:
+        return i + 1, i + 1
+    depth = 0
+    for k in range(i, len(src)):
+        depth += src[k].count("{") - src[k].count("}")
+        if depth <= 0 and k > i:
+            return i + 1, k + 1
+    return i + 1, len(src)
 
 
 def main():
     from math import comb
     path, name = sys.argv[1], sys.argv[2]
     pmc = json.load(open(sys.argv[3])).get(sys.argv[4]) if len(sys.argv) > 4 else None
+    # path frequencies per wave-step (BOTE_PSTATS=<pathstats json>): the rare
+    # regions and the no-lines client loop are weighted by them; without it,
+    # every rare region weighs 0 as before
+    pst = json.load(open(os.environ["BOTE_PSTATS"]))["per_step"] if os.environ.get("BOTE_PSTATS") else {}
     R, n, trips = (int(x) for x in sys.argv[5:8]) if len(sys.argv) > 7 else (64, 7, 4)
     groups, steps = comb(R - 3, n - 3), comb(R, n) / 64.0  # groups: the fixed parts above position 3
     per_step_groups = groups / steps
@@ -55,6 +102,8 @@ def main():
     # the sample launch's per-chunk minima (a.smin): not run by the sweep launch
     sm0 = next(i + 1 for i, l in enumerate(src) if "if (a.smin) {" in l)
     sm1 = next(i + 1 for i, l in enumerate(src) if i + 1 > sm0 and "} else if (!ABLATE(a, 4)) {" in l)
+    regions = [(region_lines(src, m), pst.get(name, 0.0)) for m, name in RARE_REGIONS]
+    blk_src = defaultdict(Counter)  # bote_group.hip source lines per block
     blk_ops = defaultdict(list)
     blk_lines = defaultdict(Counter)
     merge_blk = set()
@@ -65,6 +114,8 @@ def main():
             order.append(b)
         blk_ops[b].append(op)
         own_line[b] |= raw_ln > 0
+        if raw_ln > 0:
+            blk_src[b][raw_ln] += 1
         if wt0 <= raw_ln <= wt1 or sm0 <= raw_ln < sm1:
             merge_blk.add(b)
         if ln:
@@ -109,9 +160,22 @@ def main():
         c = Counter(classify(o) for o in blk_ops[b])
         static[s].update(c)
         # (top-K blocks made only of header code: the merge's inlined binary searches)
-        rare = (b in merge_blk or any(m in o for o in blk_ops[b] for m in RARE_MARK) or
+        rare = (b in merge_blk or any(is_rare_op(o) for o in blk_ops[b]) or
                 (s.startswith("top-K") and not own_line[b]))
-        if s.startswith("setup") or s == "other" or rare:
+        # the innermost rare region holding most of the block's source lines
+        reg = None
+        if blk_src[b]:
+            for (r0, r1), fr in regions:
+                inside = sum(c for ln_, c in blk_src[b].items() if r0 <= ln_ <= r1)
+                if inside * 2 > sum(blk_src[b].values()) and (reg is None or r1 - r0 < reg[0][1] - reg[0][0]):
+                    reg = ((r0, r1), fr)
+        if s.startswith("setup") or s == "other":
+            w = 0.0
+        elif pst and b in merge_blk and not (sm0 <= min(blk_src[b] or [0]) < sm1):
+            w = pst.get("block top-K merge", 0.0)  # (wave_topk under the lock)
+        elif pst and reg is not None:
+            w = reg[1]
+        elif rare:
             w = 0.0
         elif s in ("group precompute", "next group"):
             w = per_step_groups
@@ -119,6 +183,8 @@ def main():
             # (the other variants' bodies and the remainder loops: 0)
             other_body = b != hot and (adds[b] > 0 or b in big)
             w = float(trips) if b == hot else (1.0 if b in run and not other_body else 0.0)
+            if pst and b == hot:
+                w *= 1.0 - pst.get("no client lines", 0.0)
         else:
             w = 1.0
         for k, v in c.items():

@@ -18,6 +18,7 @@
 #            PWLS (default WL), to gpurun_out/$TAG/<workload>/
 #   trace    rocprofv3 kernel trace + stats (no counters) of bench.py for each workload in TWLS
 #   pmc      extra PMC passes: PASSES="ctr ...;ctr ..." over bench.py BENCH_ARGS
+#   shardsteps  scripts/shard_steps.py (a shard's step: wall, kernel, outside) per VARIANTS, + a trace
 #   shards   kernel trace of scripts/shard_ablate.py (per-dispatch cost of shards)
 #   ablate   scripts/ablate.py masks ABL on the -DBOTE_ABLATION library (lib_abl)
 #   pstats   scripts/pathstats.py on the -DBOTE_PATHSTATS library (lib_pstats), for each workload in WLS
@@ -121,6 +122,19 @@ step_shards() {
   timeout -k 10 180 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/shards" -o run -- \
     python3 scripts/shard_ablate.py ${SHARD_ARGS:-0} > "$O/shards.log" 2>&1 || fail shards $? "$O/shards.log"
   echo "shards ok: $(grep ablate "$O/shards.log" | tr '\n' ' ')"
+}
+
+step_shardsteps() {  # scripts/shard_steps.py per variant in VARIANTS, then a kernel trace of the default build
+  export TMPDIR=/tmp
+  for V in ${VARIANTS:-default}; do
+    if [ "$V" = default ]; then unset BOTE_LIB_PATH; else export BOTE_LIB_PATH=fantoch_amd/$V/libbote_hip.so; fi
+    timeout -k 10 180 python -u scripts/shard_steps.py 20 > "$O/shardsteps_$V.log" 2>&1 || fail "shardsteps $V" $? "$O/shardsteps_$V.log"
+    echo "shardsteps $V: $(grep -o '"parts": [0-9]*\|"step_ms": [0-9.]*\|"outside_ms": [0-9.]*' "$O/shardsteps_$V.log" | tr '\n' ' ')"
+  done
+  unset BOTE_LIB_PATH
+  timeout -k 10 180 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/shardsteps_trace" -o run -- \
+    python3 scripts/shard_steps.py 5 > "$O/shardsteps_trace.log" 2>&1 || fail shardsteps_trace $? "$O/shardsteps_trace.log"
+  echo "shardsteps trace ok"
 }
 
 step_ablate() {

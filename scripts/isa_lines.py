@@ -38,6 +38,7 @@ def parse(path, name, raw=False):
     cur_file, cur_line, main_line = 0, 0, 0
     out = []  # (main-file line, block label, op)
     block = "entry"
+    sub = 0
     for l in lines[start + 1:]:
         s = l.strip()
         if s.startswith(".Lfunc_end"):
@@ -56,6 +57,12 @@ def parse(path, name, raw=False):
             continue
         out.append((main_line, block, s.split()[0]) if not raw else
                    (main_line, block, s.split()[0], cur_line if files.get(cur_file, "").endswith("bote_group.hip") else 0))
+        if s.startswith("s_cbranch"):
+            # a conditional branch ends the basic block: the fall-through is a
+            # block of its own (e.g. the code a divergent `if` runs only when
+            # some lane takes it), even without a label
+            sub += 1
+            block = f"{block.split('+')[0]}+{sub}"
     return out
 
 

@@ -57,7 +57,7 @@ def dump(lists, K, order):
     return out, bound
 
 
-WIDE_HEAD, WIDE_SLACK, WIDE_RANK_MAX = 2, 32, 1024
+WIDE_HEAD, WIDE_SLACK, WIDE_RANK_MAX, WIDE_FEW = 2, 32, 1024, 64
 ONES = 2**64 - 1
 
 
@@ -92,6 +92,11 @@ def wide_select(values, need, slack=WIDE_SLACK, stop_early=True):
         s_hi = s_lo
         if s_hi == 0 or (stop_early and inbin - left <= slack):
             break
+        if inbin <= WIDE_FEW:  # one wave finishes a small bin exactly
+            few = sorted(v for v in values if ((v - mn) >> s_hi) == prefix)
+            x = few[left - 1]
+            lt, le = sum(1 for v in few if v < x), sum(1 for v in few if v <= x)
+            return x, left - lt, le - lt, True
     x = (prefix << s_hi) | ((1 << s_hi) - 1)
     return min(ONES, mn + x), left, inbin, s_hi == 0
 
@@ -297,3 +302,22 @@ def test_heavy_ties_at_the_kth_key_are_bounded_by_rank(blocks):
         assert keys_only > WIDE_RANK_MAX  # the key bound alone: every list's ties
     got = wide_merge(dumped, K, kb, 4096 - K)
     assert got == sorted(r for L in lists for r in L)[:K]
+
+
+@pytest.mark.parametrize("seed", range(20))
+def test_wide_select_finds_a_valid_bound(seed):
+    """wide_select's value x has at least `need` values at or below it; with
+    the early stop off it is exactly the need-th least value (any path: the
+    radix passes, a one-wave finish of a small bin, a single distinct value)."""
+    rng = random.Random(300 + seed)
+    n = rng.choice([1, 5, 100, 2000])
+    spread = rng.choice([1, 7, 1000, 2**40, 2**63])
+    vals = [rng.randrange(spread) + rng.choice([0, 2**62]) for _ in range(n)]
+    need = rng.randrange(1, n + 1)
+    x, left, inbin, exact = wide_select(vals, need, stop_early=False)
+    srt = sorted(vals)
+    assert x == srt[need - 1]
+    assert exact and inbin == vals.count(x)
+    assert sum(1 for v in vals if v < x) + left == need
+    y = wide_select(vals, need)[0]
+    assert sum(1 for v in vals if v <= y) >= need
