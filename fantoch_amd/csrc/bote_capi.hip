@@ -1179,7 +1179,13 @@ static int launch_generic(bote_sweep* s, uint64_t rb, uint64_t re, hipStream_t s
 #define BOTE_SEED_PER_WAVE 1  // sample minima per wave (4,096 slots) instead of per chunk (32,768)
 #endif
 #ifndef BOTE_SEED_STEPS
-#define BOTE_SEED_STEPS 8  // sample steps per wave (r03v A/B: 8 vs 1, kernel -1.6 %, 1/8 shard -5 %)
+// sample steps per wave on a full range (r03v A/B: 8 vs 1, kernel -1.6 %, 1/8
+// shard -5 %; r05g: 4 and 8 give the same R=64 n=7 step, 14.15-14.17 vs
+// 14.16-14.25 ms, and 4 halves the sample launch: 0.14 vs 0.18 ms outside the kernel)
+#define BOTE_SEED_STEPS 4
+#endif
+#ifndef BOTE_SEED_SCALE
+#define BOTE_SEED_SCALE 1  // scale the sample steps with the launch's share of the rank space
 #endif
 #ifndef BOTE_SEED_RUN
 #define BOTE_SEED_RUN 1  // consecutive steps per sample chunk (one group precompute per chunk)
@@ -1192,8 +1198,20 @@ static int sample_seed(bote_sweep* s, bote::FastArgs& f, uint64_t rb, uint64_t r
   // kernel 15.52 vs 15.35 ms, their K least minima are a looser bound, r03x.)
   const uint64_t fit = (re - rb) / (64 * 8);
   const uint32_t ssteps = BOTE_SEED_RUN;
+  // sample steps per wave: BOTE_SEED_STEPS on a full sweep; a shard's launch
+  // scales them by sqrt(its share of the rank space), rounded up
+  // (BOTE_SEED_SCALE): the sample costs ~ steps, the block merges it saves
+  // ~ range / steps, so the best count grows as sqrt(range).  r05g, R=64 n=7
+  // shards, 8 scaled (8 / 3 / 1 steps) against 8 fixed: 1/8 shard 2.089 vs
+  // 2.125 ms per step, 1/64 0.492 vs 0.531 ms
+  uint32_t steps = BOTE_SEED_STEPS;
+  if (BOTE_SEED_SCALE) {
+    const double share = (double)(re - rb) / (double)binom_u64(s->ns, s->n);
+    steps = (uint32_t)std::max(1.0, std::min((double)BOTE_SEED_STEPS,
+                                             std::ceil(BOTE_SEED_STEPS * std::sqrt(share) - 1e-9)));
+  }
   const uint32_t nsamp = (uint32_t)std::min<uint64_t>(
-      {(uint64_t)base * std::max(1, BOTE_SEED_STEPS / BOTE_SEED_RUN), std::max<uint64_t>(base, fit / ssteps), 65536});
+      {(uint64_t)base * std::max<uint32_t>(1, steps / BOTE_SEED_RUN), std::max<uint64_t>(base, fit / ssteps), 65536});
   if (nsamp < s->K || re - rb < (uint64_t)nsamp * ssteps * 64 * 8) return BOTE_OK;
   auto key = std::make_pair(rb, re);
   auto it = s->samples.find(key);

@@ -818,9 +818,14 @@ __device__ __forceinline__ bool is_rec_max(const Rec& r) { return r.key == ~0ull
 static_assert(WIDE_MERGE_LISTS == (uint32_t)(WIDE_BD * WIDE_LISTS_PER_THREAD), "one thread per WIDE_LISTS_PER_THREAD lists");
 static_assert(WIDE_BINS == WIDE_BD, "the digit histogram shares the scan array");
 constexpr int WIDE_FEW = 64;  // a bin this small is finished by one wave (wide_select)
+// LDS: the head records of every list (thread-minor; the windowed path's
+// sort buffer reuses them), the one-pass gather, the scan / digit histogram,
+// control words, per-wave reductions and a small bin's values: 149 KB
+constexpr size_t WIDE_HEADS_BYTES = (size_t)WIDE_LISTS_PER_THREAD * WIDE_HEAD * WIDE_BD * 16;
+static_assert(WIDE_HEADS_BYTES >= (size_t)WIDE_SORT * 16, "the windowed sort buffer fits the head records");
 size_t merge_wide_smem() {
-  return (size_t)WIDE_SORT * sizeof(Rec) + (WIDE_BD + 8) * sizeof(uint32_t) + 4 * WIDE_WAVES * sizeof(uint64_t) +
-         WIDE_FEW * sizeof(uint64_t);
+  return WIDE_HEADS_BYTES + (size_t)WIDE_RANK_MAX * 16 + (WIDE_BD + 8) * sizeof(uint32_t) +
+         4 * WIDE_WAVES * sizeof(uint64_t) + WIDE_FEW * sizeof(uint64_t);
 }
 
 // inclusive prefix sum over the wavefront
@@ -971,6 +976,14 @@ __global__ void __launch_bounds__(WIDE_BD) merge_wide_kernel(const Rec* src, uin
                                                              const unsigned long long* kbound, uint32_t K,
                                                              const unsigned long long* csrc,
                                                              const unsigned long long* calt, uint64_t* cdst) {
+#ifdef BOTE_MERGE_PRINTF
+  const uint64_t T0 = wall_clock64();
+  uint64_t TT[4] = {0, 0, 0, 0};
+  int tn = 0;
+#define WIDE_T(name) TT[tn++ & 3] = wall_clock64() - T0;
+#else
+#define WIDE_T(name)
+#endif
   const bool use_alt = sel && *sel > cap;
   if (use_alt) {  // device-side choice of the input (fast sweep overflow fallback)
     src = alt;
@@ -980,8 +993,10 @@ __global__ void __launch_bounds__(WIDE_BD) merge_wide_kernel(const Rec* src, uin
   // pick_counters_kernel does for the merge tree; one launch fewer)
   if (cdst && blockIdx.x == 0 && threadIdx.x < 2) cdst[threadIdx.x] = (use_alt ? calt : csrc)[threadIdx.x];
   extern __shared__ __align__(16) unsigned char wsm[];
-  Rec* buf = (Rec*)wsm;
-  uint32_t* scan = (uint32_t*)(wsm + (size_t)WIDE_SORT * sizeof(Rec));  // also the digit histogram
+  Rec* hr = (Rec*)wsm;                              // head records (then the windowed path's buffer)
+  Rec* buf = hr;                                    // the windowed path's sort buffer
+  Rec* gbuf = (Rec*)(wsm + WIDE_HEADS_BYTES);       // the one-pass gather
+  uint32_t* scan = (uint32_t*)(wsm + WIDE_HEADS_BYTES + (size_t)WIDE_RANK_MAX * 16);  // also the digit histogram
   uint32_t* ctl = scan + WIDE_BD;  // [0] next window start, [1] records this pass; [2..4] the digit pick
   uint64_t* red = (uint64_t*)(ctl + 8);  // per wave: least and greatest value, count
   const uint32_t o = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -997,16 +1012,24 @@ __global__ void __launch_bounds__(WIDE_BD) merge_wide_kernel(const Rec* src, uin
   // records above the bound on the K-th key (the least K-th key of the
   // group blocks' full lists) cannot be among the K least of the union
   const uint64_t b0 = kbound && !use_alt ? kbound[o] : ~0ull;
-  // the keys of the first WIDE_HEAD records of all of a thread's lists load
-  // together into LDS (the gather buffer, free until the gather; in
-  // registers they spilled at 1,024 threads), thread-minor: conflict-free
-  static_assert(WIDE_LISTS_PER_THREAD * WIDE_HEAD * 8 <= 16 * WIDE_SORT / WIDE_BD, "head keys fit the gather buffer");
-  uint64_t* hkl = (uint64_t*)buf;
-  auto hk = [&](int j, int c) -> uint64_t& { return hkl[(c * LT + j) * WIDE_BD + tid]; };
+  // the first WIDE_HEAD records of all of a thread's lists load together
+  // (one round trip to memory: the lists were written by blocks on every
+  // XCD) into LDS, thread-minor (in registers they spilled at 1,024
+  // threads); everything up to the gather then reads LDS
+  auto hrec = [&](int j, int c) -> Rec& { return hr[(c * LT + j) * WIDE_BD + tid]; };
+  auto hk = [&](int j, int c) -> uint64_t { return hrec(j, c).key; };
+  {
+    Rec t[LT][H];
 #pragma unroll
-  for (int j = 0; j < LT; ++j)
+    for (int j = 0; j < LT; ++j)
 #pragma unroll
-    for (int c = 0; c < H; ++c) hk(j, c) = live(j) && (uint32_t)c < KK ? list(j)[c].key : ~0ull;
+      for (int c = 0; c < H; ++c) t[j][c] = live(j) && (uint32_t)c < KK ? list(j)[c] : Rec{~0ull, ~0ull};
+#pragma unroll
+    for (int j = 0; j < LT; ++j)
+#pragma unroll
+      for (int c = 0; c < H; ++c) hrec(j, c) = t[j][c];
+  }
+  WIDE_T("heads")
   // the bound record (bk, br): the union's K least are at or below it
   uint64_t bk = ~0ull, br = ~0ull;
 #if BOTE_MERGE_HEADS
@@ -1032,6 +1055,7 @@ __global__ void __launch_bounds__(WIDE_BD) merge_wide_kernel(const Rec* src, uin
     // (to the exact key: a bin's worth of heads above the K-th could stand
     // for many more tied records beyond the heads)
     const WideSel ks = wide_select(each_head, KK, scan, ctl, red, false);
+    WIDE_T("keysel")
     if (!ks.none) {
       bk = ks.x;
       if (ks.inbin > 1) {
@@ -1043,17 +1067,13 @@ __global__ void __launch_bounds__(WIDE_BD) merge_wide_kernel(const Rec* src, uin
           for (int j = 0; j < LT; ++j)
 #pragma unroll
             for (int c = 0; c < H; ++c)
-              if ((uint32_t)c < hn[j] && hk(j, c) == bk) f(list(j)[c].rank);
+              if ((uint32_t)c < hn[j] && hk(j, c) == bk) f(hrec(j, c).rank);
         };
         const WideSel rs = wide_select(each_tie, ks.left, scan, ctl, red, true);
         if (!rs.none) br = rs.x;
       }
     }
-#ifdef BOTE_MERGE_PRINTF
-    if (tid == 0)
-      printf("merge o=%u lists=%u b0=%llx bk=%llx br=%llx exact=%d inbin=%u left=%u\n", o, n_lists,
-             (unsigned long long)b0, (unsigned long long)bk, (unsigned long long)br, (int)ks.exact, ks.inbin, ks.left);
-#endif
+
   }
 #endif
   const uint64_t kb = min(b0, bk);
@@ -1073,7 +1093,7 @@ __global__ void __launch_bounds__(WIDE_BD) merge_wide_kernel(const Rec* src, uin
       if (go && (uint32_t)i < KK) {
         const uint64_t k = hk(j, i);
         bool in = k <= kb;
-        if (in && (k == ~0ull || (k == bk && br != ~0ull))) in = keep(list(j)[i]);
+        if (in && (k == ~0ull || (k == bk && br != ~0ull))) in = keep(hrec(j, i));
         c += in ? 1u : 0u;
         go = in;
       } else {
@@ -1089,8 +1109,7 @@ __global__ void __launch_bounds__(WIDE_BD) merge_wide_kernel(const Rec* src, uin
     mine += c;
   }
   // exclusive scan of the threads' totals (list order = thread order): per
-  // wave by shuffles, then the waves' totals (the barrier also ends the head
-  // keys' use of the gather buffer)
+  // wave by shuffles, then the waves' totals
   const uint32_t incl = wave_incl_scan(mine);
   if (lane == 63) scan[wv] = incl;
   __syncthreads();
@@ -1103,26 +1122,37 @@ __global__ void __launch_bounds__(WIDE_BD) merge_wide_kernel(const Rec* src, uin
   }
 #pragma unroll
   for (int j = 0; j < LT; ++j) off[j] += base;
-#ifdef BOTE_MERGE_PRINTF
-  if (tid == 0) printf("merge o=%u total=%u\n", o, total);
-#endif
+  WIDE_T("scan")
   if (total <= (uint32_t)WIDE_RANK_MAX) {  // (block-uniform) one pass: slot = rank among the gathered
 #pragma unroll
     for (int j = 0; j < LT; ++j) {
-      const Rec* L = list(j);
-      for (uint32_t c = 0; c < cnt[j]; ++c) buf[off[j] + c] = L[c];
+#pragma unroll
+      for (int c = 0; c < H; ++c)
+        if ((uint32_t)c < cnt[j]) gbuf[off[j] + c] = hrec(j, c);
+      if (cnt[j] > (uint32_t)H) {  // (rare: beyond the heads)
+        const Rec* L = list(j);
+        for (uint32_t c = H; c < cnt[j]; ++c) gbuf[off[j] + c] = L[c];
+      }
     }
     __syncthreads();
     for (uint32_t i = tid; i < total; i += WIDE_BD) {
-      const Rec x = buf[i];
+      const Rec x = gbuf[i];
       uint32_t r = 0;
-      for (uint32_t m = 0; m < total; ++m) r += (uint32_t)rec_lt(buf[m], x);
+      for (uint32_t m = 0; m < total; ++m) r += (uint32_t)rec_lt(gbuf[m], x);
       if (r < KK) out[r] = x;
     }
     for (uint32_t i = min(total, KK) + tid; i < (uint32_t)KP; i += WIDE_BD) out[i] = rec_max();
+    WIDE_T("done")
+#ifdef BOTE_MERGE_PRINTF
+    if (tid == 0)
+      printf("merge o=%u lists=%u total=%u bk=%llx br=%llx ticks heads %llu keysel %llu scan %llu done %llu\n", o,
+             n_lists, total, (unsigned long long)bk, (unsigned long long)br, (unsigned long long)TT[0],
+             (unsigned long long)TT[1], (unsigned long long)TT[2], (unsigned long long)TT[3]);
+#endif
     return;
   }
-  // running K least: buf[0 .. have)
+  // running K least: buf[0 .. have) (buf overwrites the head records: the
+  // windowed passes gather from memory)
   uint32_t have = 0;
   const uint32_t room = WIDE_SORT - KK;  // records gathered per pass
   uint32_t w0 = 0;  // window start (in the concatenated order)
@@ -1219,8 +1249,10 @@ hipError_t launch_zero_ctl(unsigned long long* counters, unsigned long long* qco
 // bin.  (A bitonic sort of 4096 keys took 56 us: 78 barrier-separated stages.)
 __global__ void __launch_bounds__(1024) seed_kernel(const uint64_t* smin, uint32_t nsamp, uint32_t K, uint64_t* tseed) {
   __shared__ uint32_t hist[256];
-  __shared__ uint64_t sel[2];  // prefix, remaining rank
+  __shared__ uint64_t sel[3];  // prefix, remaining rank, keys in the chosen bin
   __shared__ uint64_t red[2][16];
+  __shared__ uint64_t few[64];  // a small final bin's keys
+  __shared__ uint32_t nfew;
   const uint32_t o = blockIdx.x, tid = threadIdx.x, BD = blockDim.x;
   if (nsamp < K || K == 0) {
     if (tid == 0) tseed[o] = ~0ull;
@@ -1321,9 +1353,37 @@ __global__ void __launch_bounds__(1024) seed_kernel(const uint64_t* smin, uint32
       if (digit >= 0) {  // exactly one lane holds the K-th key's digit
         sel[0] = (sel[0] << 8) | (uint64_t)digit;
         sel[1] = left;
+        sel[2] = hist[digit];
       }
+      if (tid == 0) nfew = 0;
     }
     __syncthreads();
+    if (pass > 0 && sel[2] <= 64) {  // (block-uniform) a small bin: one wave ranks its keys
+      const uint64_t pfx = sel[0];
+      const int shb = 8 * pass;
+      auto push = [&](uint64_t v) {
+        if ((v >> shb) == pfx) few[atomicAdd(&nfew, 1u)] = v;
+      };
+      if (inreg) {
+#pragma unroll
+        for (int i = 0; i < RP; ++i)
+          if (tid + (uint32_t)i * BD < nsamp) push(xr[i]);
+      } else {
+        for (uint32_t k = tid; k < nsamp; k += BD) push(x[k]);
+      }
+      __syncthreads();
+      if (tid < 64) {  // the sel[1]-th least of the bin's keys
+        const uint32_t nb = nfew, need = (uint32_t)sel[1];
+        const uint64_t v = tid < nb ? few[tid] : ~0ull;
+        uint32_t lt = 0, le = 0;
+        for (uint32_t j = 0; j < nb; ++j) {
+          lt += (uint32_t)(few[j] < v);
+          le += (uint32_t)(few[j] <= v);
+        }
+        if (tid < nb && lt < need && need <= le) tseed[o] = v;  // (every lane holding it writes the same)
+      }
+      return;
+    }
   }
   if (tid == 0) tseed[o] = sel[0];
 }

@@ -3,7 +3,8 @@ per 64-config step, reconciled against the measured SQ_INSTS_VALU.
 
   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -DBOTE_ISA_N7 -g \
       --offload-device-only -S -o kg.s fantoch_amd/csrc/bote_group.hip
-  python scripts/class_mix_table.py kg.s ILi7ELb1ELb1ELb1ELb0ELb0E profiles/pmc.json r64n7_n1 > profiles/<tag>_class_mix.md
+  BOTE_PSTATS=<pathstats json> python scripts/class_mix_table.py kg.s ILi7ELb1ELb1ELb1ELb0ELb1E profiles/pmc.json \
+      r64n7_n1 > profiles/<tag>_class_mix.md
   (optional 5th-7th arguments: R n trips -- the workload, and the client
   loop's unrolled-body trips per step: nq / U; default 64 7 4; the config-5
   kernel, -DBOTE_ISA_N6: ... r128n6_n1 128 6 8)
@@ -58,11 +59,14 @@ FAST_RATE, SLOW_RATE = 1.6, 0.95
 # region that holds most of its bote_group.hip lines.
 RARE_REGIONS = [
     ("if (amb) {  // exact re-scan", "leader re-scan"),
+    ("PSTAT(a, 3, amb);", "leader deferred"),
+    ("if (vlead == 0.0 && Va == 0) continue;", "both COV zero (not counted: ~0)"),
     ("mok = (mom_mean(mf) - mom_mean(ma)) >= a.p_fmean;", "f64 mean test f=1"),
     ("if (defer) {", "validity deferred"),
-    ("PSTAT(a, 9, maybe);", "f64 score"),
-    ("PSTAT(a, 10, maybe);", "COV af1 key"),
 ]
+# (the f64 score and COV af1 key bodies hold f64 arithmetic, so their blocks
+# are rare by their ops; as line regions they would also take in blocks the
+# compiler sinks there, e.g. the digest, whose .loc lines say 1704)
 
 
 def region_lines(src, marker):
@@ -76,9 +80,10 @@ def region_lines(src, marker):
         return i + 1, i + 1
     depth = 0
     for k in range(i, len(src)):
-        depth += src[k].count("{") - src[k].count("}")
-        if depth <= 0 and k > i:
-            return i + 1, k + 1
+        for ch in src[k]:  # (character by character: `} else {` closes the region)
+            depth += 1 if ch == "{" else (-1 if ch == "}" else 0)
+            if depth == 0 and ch == "}":
+                return i + 1, k + 1
     return i + 1, len(src)
 
 
@@ -114,8 +119,8 @@ def main():
             order.append(b)
         blk_ops[b].append(op)
         own_line[b] |= raw_ln > 0
-        if raw_ln > 0:
-            blk_src[b][raw_ln] += 1
+        if ln:  # (the kernel-body line: inlined helpers count at their call site)
+            blk_src[b][ln] += 1
         if wt0 <= raw_ln <= wt1 or sm0 <= raw_ln < sm1:
             merge_blk.add(b)
         if ln:
@@ -135,6 +140,16 @@ def main():
         # LDS adds (the epilogue after it has the most v_dot2 but runs once)
         big = [b for b in loop_blocks if adds[b] >= 8]
     hot = min(big, key=lambda b: sum(1 for o in blk_ops[b] if o.startswith("ds_"))) if big else None
+    nolines = None
+    # BIN with the flush-free loops (round 5): four bodies -- lines / no
+    # lines, each with and without the flush.  The bench's one 32-bit sum
+    # holds every client, so the flush-free bodies run: the lines body (4
+    # quads, 16 LDS adds per iteration) and the no-lines body (2 quads, 8 adds)
+    FLUSH_OPS = ("v_lshl_add_u64", "v_add_co_u32_e32", "v_addc_co_u32_e32", "v_cndmask_b32_e32", "v_cndmask_b32_e64")
+    nf = [b for b in big if adds[b] >= 8 and not any(o in FLUSH_OPS for o in blk_ops[b])]
+    if len(nf) >= 2:
+        hot = max(nf, key=lambda b: adds[b])
+        nolines = min(nf, key=lambda b: adds[b])
     run = set()
     if hot and any(adds[b] >= 8 for b in loop_blocks):
         # BIN: once per step, the blocks between the lines body and the next
@@ -185,6 +200,10 @@ def main():
             w = float(trips) if b == hot else (1.0 if b in run and not other_body else 0.0)
             if pst and b == hot:
                 w *= 1.0 - pst.get("no client lines", 0.0)
+            elif pst and b == nolines:
+                # the no-lines body (2 quads per iteration: twice the lines
+                # body's trips) on the steps with more pairs than line slots
+                w = 2.0 * trips * pst.get("no client lines", 0.0)
         else:
             w = 1.0
         for k, v in c.items():
@@ -222,9 +241,13 @@ def main():
         real = sum(comb(ns - 1 - p3, n - 4) * ceil(comb(p3, 3) / 64) for p3 in range(3, ns)) / (comb(ns, n) / 64)
         print(f"Measured SQ_INSTS_VALU per 64 configs ({pmc['source']}): **{meas:.0f}**.  Groups run "
               f"{real:.3f} steps per 64 configs (partial last steps), so the model accounts for "
-              f"{model * real:.0f} = {model * real / meas:.0%} of it; the rest is the rare paths (f64 "
-              f"decisions inside their bands, leader re-scans, block top-K merges), which run for a whole "
-              f"wavefront when any lane takes them, and per-chunk work.")
+              f"{model * real:.0f} = {model * real / meas:.0%} of it.  "
+              + (f"Rare paths (f64 decisions inside their bands, leader re-scans, block top-K merges, the "
+                 f"no-lines loop) are weighted by their measured frequency per wave-step "
+                 f"({os.environ['BOTE_PSTATS']}); per-chunk setup counts 0."
+                 if pst else
+                 "The rest is the rare paths (f64 decisions inside their bands, leader re-scans, block top-K "
+                 "merges), which run for a whole wavefront when any lane takes them, and per-chunk work."))
         ceil = 1.0 / (tot["valu_fast"] / model / FAST_RATE + (1 - tot["valu_fast"] / model) / SLOW_RATE) / 2.0
         print(f"Issue ceiling of this mix: {ceil:.1%} of the 2-cycle nominal rate; measured "
               f"{pmc['valu_issue_util']:.1%} ({pmc['valu_issue_util'] / ceil:.0%} of the ceiling).")
