@@ -1486,6 +1486,11 @@ int bote_sweep_destroy(bote_sweep* s) {
   DevGuard dev_guard;  // the caller's current device is restored on return
   if (!s) return BOTE_OK;
   (void)hipSetDevice(s->p ? s->p->device : 0);
+  // work the last launch enqueued may still run (a launch without a result
+  // call): drain the device before its buffers are freed and handed to the
+  // next allocation (the device, not last_stream: the caller's stream may be
+  // gone by now)
+  if (s->launched) (void)hipDeviceSynchronize();
   for (auto& e : s->evpool) {
     (void)hipEventDestroy(e.first);
     (void)hipEventDestroy(e.second);

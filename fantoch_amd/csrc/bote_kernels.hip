@@ -825,7 +825,7 @@ constexpr size_t WIDE_HEADS_BYTES = (size_t)WIDE_LISTS_PER_THREAD * WIDE_HEAD * 
 static_assert(WIDE_HEADS_BYTES >= (size_t)WIDE_SORT * 16, "the windowed sort buffer fits the head records");
 size_t merge_wide_smem() {
   return WIDE_HEADS_BYTES + (size_t)WIDE_RANK_MAX * 16 + (WIDE_BD + 8) * sizeof(uint32_t) +
-         4 * WIDE_WAVES * sizeof(uint64_t) + WIDE_FEW * sizeof(uint64_t);
+         4 * WIDE_WAVES * sizeof(uint64_t) + 2 * WIDE_FEW * sizeof(uint64_t);
 }
 
 // inclusive prefix sum over the wavefront
@@ -851,13 +851,16 @@ struct WideSel {
   uint64_t x;
   uint32_t left, inbin;
   bool exact, none;
+  bool has_aux;  // a small final bin was ranked by (value, aux): aux is the selected item's
+  uint64_t aux;
 };
 template <class Each>
 __device__ WideSel wide_select(Each each, uint64_t need, uint32_t* hist, uint32_t* ctl, uint64_t* red, bool slack) {
   const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   uint64_t* few = red + 4 * WIDE_WAVES;  // the values of a small final bin
+  uint64_t* fewa = few + WIDE_FEW;       // and their aux words (ranks: the items are then distinct)
   uint64_t mn = ~0ull, mx = 0, nv = 0;
-  each([&](uint64_t v) {
+  each([&](uint64_t v, uint64_t) {
     mn = min(mn, v);
     mx = max(mx, v);
     ++nv;
@@ -883,11 +886,11 @@ __device__ WideSel wide_select(Each each, uint64_t need, uint32_t* hist, uint32_
     mx = max(mx, red[WIDE_WAVES + w]);
     nv += red[2 * WIDE_WAVES + w];
   }
-  WideSel r{~0ull, 0, 0, false, true};
+  WideSel r{~0ull, 0, 0, false, true, false, 0};
   if (nv >= need && need > 0) {  // (block-uniform)
     r.none = false;
     if (mx == mn) {
-      r = WideSel{mn, (uint32_t)need, (uint32_t)nv, true, false};
+      r = WideSel{mn, (uint32_t)need, (uint32_t)nv, true, false, false, 0};
     } else {
       uint32_t s_hi = 64 - (uint32_t)__clzll(mx - mn);  // every (v - mn) < 2^s_hi
       uint64_t prefix = 0;
@@ -895,7 +898,7 @@ __device__ WideSel wide_select(Each each, uint64_t need, uint32_t* hist, uint32_
         const uint32_t s_lo = s_hi > 10 ? s_hi - 10 : 0, w = s_hi - s_lo;
         hist[tid] = 0;
         __syncthreads();
-        each([&](uint64_t v) {
+        each([&](uint64_t v, uint64_t) {
           v -= mn;
           if (s_hi >= 64 || (v >> s_hi) == prefix) atomicAdd(&hist[(uint32_t)(v >> s_lo) & ((1u << w) - 1)], 1u);
         });
@@ -931,29 +934,44 @@ __device__ WideSel wide_select(Each each, uint64_t need, uint32_t* hist, uint32_
           break;
         }
         if (inbin <= (uint32_t)WIDE_FEW) {  // (block-uniform) the bin's values to one wave: exact
-          each([&](uint64_t v) {
+          each([&](uint64_t v, uint64_t aux) {
             v -= mn;
-            if ((v >> s_hi) == prefix) few[atomicAdd(&ctl[5], 1u)] = v;
+            if ((v >> s_hi) == prefix) {
+              const uint32_t k = atomicAdd(&ctl[5], 1u);
+              few[k] = v;
+              fewa[k] = aux;
+            }
           });
           __syncthreads();
           if (wv == 0) {
-            // the left-th least: the value with fewer than `left` values below it
-            // and at least `left` at or below it (ties: every lane holding it agrees)
-            const uint64_t x = lane < inbin ? few[lane] : ~0ull;
-            uint32_t lt = 0, le = 0;
-            for (uint32_t j = 0; j < inbin; ++j) {
-              const uint64_t y = few[j];
-              lt += (uint32_t)(y < x);
-              le += (uint32_t)(y <= x);
+            // the left-th least item in (value, aux) order: fewer than `left`
+            // items below it and at least `left` at or below it (equal items:
+            // every lane holding one agrees); with distinct aux words (ranks)
+            // it is one item, so the caller has its aux without a second select
+            const uint64_t x = lane < inbin ? few[lane] : ~0ull, xa = lane < inbin ? fewa[lane] : ~0ull;
+            uint32_t lt = 0, le = 0, vlt = 0, vle = 0;
+            for (uint32_t j = 0; j < inbin; j += 4) {  // (4 reads in flight; inbin <= 64 = the buffer)
+#pragma unroll
+              for (uint32_t u = 0; u < 4; ++u) {
+                const uint64_t y = few[j + u], ya = fewa[j + u];
+                const bool in = j + u < inbin;
+                lt += (uint32_t)(in && (y < x || (y == x && ya < xa)));
+                le += (uint32_t)(in && (y < x || (y == x && ya <= xa)));
+                vlt += (uint32_t)(in && y < x);
+                vle += (uint32_t)(in && y <= x);
+              }
             }
             if (lane < inbin && lt < left && left <= le) {
               red[0] = x;
-              ctl[3] = left - lt;  // (its position among the values equal to it)
-              ctl[4] = le - lt;
+              red[1] = xa;
+              ctl[3] = left - vlt;  // (its position among the values equal to it)
+              ctl[4] = vle - vlt;
             }
           }
           __syncthreads();
           r.x = mn + red[0];
+          r.aux = red[1];
+          r.has_aux = true;
           r.left = ctl[3];
           r.inbin = ctl[4];
           r.exact = true;
@@ -1050,7 +1068,7 @@ __global__ void __launch_bounds__(WIDE_BD) merge_wide_kernel(const Rec* src, uin
       for (int j = 0; j < LT; ++j)
 #pragma unroll
         for (int c = 0; c < H; ++c)
-          if ((uint32_t)c < hn[j]) f(hk(j, c));
+          if ((uint32_t)c < hn[j]) f(hk(j, c), hrec(j, c).rank);
     };
     // (to the exact key: a bin's worth of heads above the K-th could stand
     // for many more tied records beyond the heads)
@@ -1058,7 +1076,9 @@ __global__ void __launch_bounds__(WIDE_BD) merge_wide_kernel(const Rec* src, uin
     WIDE_T("keysel")
     if (!ks.none) {
       bk = ks.x;
-      if (ks.inbin > 1) {
+      if (ks.has_aux && ks.inbin > 1) {
+        br = ks.aux;  // (a small final bin ranked by (key, rank): the K-th head record itself)
+      } else if (ks.inbin > 1) {
         // heads tie at the K-th key (FPaxos means: round 5 measured 1,186
         // records at one key on a 1/8 shard): the left-th least rank among
         // them makes (bk, br) the K-th least head record itself
@@ -1067,7 +1087,7 @@ __global__ void __launch_bounds__(WIDE_BD) merge_wide_kernel(const Rec* src, uin
           for (int j = 0; j < LT; ++j)
 #pragma unroll
             for (int c = 0; c < H; ++c)
-              if ((uint32_t)c < hn[j] && hk(j, c) == bk) f(hrec(j, c).rank);
+              if ((uint32_t)c < hn[j] && hk(j, c) == bk) f(hrec(j, c).rank, 0ull);
         };
         const WideSel rs = wide_select(each_tie, ks.left, scan, ctl, red, true);
         if (!rs.none) br = rs.x;
@@ -1134,11 +1154,18 @@ __global__ void __launch_bounds__(WIDE_BD) merge_wide_kernel(const Rec* src, uin
         for (uint32_t c = H; c < cnt[j]; ++c) gbuf[off[j] + c] = L[c];
       }
     }
+    // (padded with rec_max to a multiple of 8: the count loop below keeps 8
+    // independent LDS reads in flight; padding is never below a record)
+    const uint32_t tot8 = (total + 7) & ~7u;
+    if (tid >= total && tid < tot8) gbuf[tid] = rec_max();
     __syncthreads();
     for (uint32_t i = tid; i < total; i += WIDE_BD) {
       const Rec x = gbuf[i];
       uint32_t r = 0;
-      for (uint32_t m = 0; m < total; ++m) r += (uint32_t)rec_lt(gbuf[m], x);
+      for (uint32_t m = 0; m < tot8; m += 8) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) r += (uint32_t)rec_lt(gbuf[m + u], x);
+      }
       if (r < KK) out[r] = x;
     }
     for (uint32_t i = min(total, KK) + tid; i < (uint32_t)KP; i += WIDE_BD) out[i] = rec_max();
@@ -1376,9 +1403,13 @@ __global__ void __launch_bounds__(1024) seed_kernel(const uint64_t* smin, uint32
         const uint32_t nb = nfew, need = (uint32_t)sel[1];
         const uint64_t v = tid < nb ? few[tid] : ~0ull;
         uint32_t lt = 0, le = 0;
-        for (uint32_t j = 0; j < nb; ++j) {
-          lt += (uint32_t)(few[j] < v);
-          le += (uint32_t)(few[j] <= v);
+        for (uint32_t j = 0; j < nb; j += 4) {  // (4 reads in flight; nb <= 64 = the buffer)
+#pragma unroll
+          for (uint32_t u = 0; u < 4; ++u) {
+            const uint64_t y = few[j + u];
+            lt += (uint32_t)(j + u < nb && y < v);
+            le += (uint32_t)(j + u < nb && y <= v);
+          }
         }
         if (tid < nb && lt < need && need <= le) tseed[o] = v;  // (every lane holding it writes the same)
       }

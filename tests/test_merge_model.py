@@ -61,16 +61,20 @@ WIDE_HEAD, WIDE_SLACK, WIDE_RANK_MAX, WIDE_FEW = 2, 32, 1024, 64
 ONES = 2**64 - 1
 
 
-def wide_select(values, need, slack=WIDE_SLACK, stop_early=True):
+def wide_select(values, need, slack=WIDE_SLACK, stop_early=True, aux=None):
     """merge_wide_kernel's wide_select: a value x with at least `need` values
     <= x, by a radix select with 10-bit digits over (v - least) that stops
     once the chosen bin holds at most `slack` values beyond the need-th, or at
-    the exact value.  Returns (x, left, inbin, exact) or None (too few)."""
+    the exact value.  Returns (x, left, inbin, exact, aux) or None (too few):
+    a final bin of <= WIDE_FEW values is ranked by (value, aux) and `aux` is
+    the selected item's aux word (None when the passes ended the select)."""
+    if aux is None:
+        aux = [0] * len(values)
     if len(values) < need or need == 0:
         return None
     mn, mx = min(values), max(values)
     if mn == mx:
-        return mn, need, len(values), True
+        return mn, need, len(values), True, None
     s_hi = (mx - mn).bit_length()
     prefix = 0
     while True:
@@ -92,13 +96,13 @@ def wide_select(values, need, slack=WIDE_SLACK, stop_early=True):
         s_hi = s_lo
         if s_hi == 0 or (stop_early and inbin - left <= slack):
             break
-        if inbin <= WIDE_FEW:  # one wave finishes a small bin exactly
-            few = sorted(v for v in values if ((v - mn) >> s_hi) == prefix)
-            x = few[left - 1]
-            lt, le = sum(1 for v in few if v < x), sum(1 for v in few if v <= x)
-            return x, left - lt, le - lt, True
+        if inbin <= WIDE_FEW:  # one wave finishes a small bin exactly, by (value, aux)
+            few = sorted((v, a) for v, a in zip(values, aux) if ((v - mn) >> s_hi) == prefix)
+            x, xa = few[left - 1]
+            lt, le = sum(1 for v, _ in few if v < x), sum(1 for v, _ in few if v <= x)
+            return x, left - lt, le - lt, True, xa
     x = (prefix << s_hi) | ((1 << s_hi) - 1)
-    return min(ONES, mn + x), left, inbin, s_hi == 0
+    return min(ONES, mn + x), left, inbin, s_hi == 0, None
 
 
 def head_bound(dumped, K, b0, H=WIDE_HEAD, slack=WIDE_SLACK):
@@ -115,12 +119,14 @@ def head_bound(dumped, K, b0, H=WIDE_HEAD, slack=WIDE_SLACK):
             if r == REC_MAX or r[0] == ONES or r[0] > b0:
                 break
             heads.append(r)
-    ks = wide_select([k for k, _ in heads], K, slack, stop_early=False)
+    ks = wide_select([k for k, _ in heads], K, slack, stop_early=False, aux=[rk for _, rk in heads])
     if ks is None:
         return ONES, ONES
-    bk, left, inbin, exact = ks
+    bk, left, inbin, exact, kaux = ks
     br = ONES
-    if inbin > 1:
+    if kaux is not None and inbin > 1:
+        br = kaux  # (the small final bin ranked by (key, rank): the K-th head record)
+    elif inbin > 1:
         rs = wide_select([rk for k, rk in heads if k == bk], left, slack)
         if rs is not None:
             br = rs[0]
@@ -314,7 +320,7 @@ def test_wide_select_finds_a_valid_bound(seed):
     spread = rng.choice([1, 7, 1000, 2**40, 2**63])
     vals = [rng.randrange(spread) + rng.choice([0, 2**62]) for _ in range(n)]
     need = rng.randrange(1, n + 1)
-    x, left, inbin, exact = wide_select(vals, need, stop_early=False)
+    x, left, inbin, exact, _ = wide_select(vals, need, stop_early=False)
     srt = sorted(vals)
     assert x == srt[need - 1]
     assert exact and inbin == vals.count(x)
