@@ -210,11 +210,16 @@ def main_gcp(args):
     sweeps = [Sweep(dp, srv, srv, n, DEFAULT_OBJECTIVES, K=100, ranking=DEFAULT_RANKING, digest=True) for n in GCP_NS]
     stream = torch.cuda.current_stream().cuda_stream
     total = sum(sw.total for sw in sweeps)
+    # every sweep's result block goes to its own pinned buffer on the stream;
+    # one synchronisation per step, then the host parses the six blocks
+    hosts = [torch.empty(sw.result_bytes(), dtype=torch.uint8, pin_memory=True) for sw in sweeps]
 
     def step():
-        for sw in sweeps:
+        for sw, h in zip(sweeps, hosts):
             sw.launch(0, sw.total, stream)
-        return [sw.result(stream) for sw in sweeps]
+            sw.result_device(h.data_ptr(), stream)
+        torch.cuda.current_stream().synchronize()
+        return [sw.parse_block(h.numpy()) for sw, h in zip(sweeps, hosts)]
 
     for _ in range(args.warmup):
         res = step()

@@ -885,14 +885,17 @@ int bote_sweep_create_keys(const bote_planet* p, const uint32_t* servers, uint32
     if (kernel == BOTE_KERNEL_GROUP && !want_group) return cleanup(fail(BOTE_E_ARG, "group kernel needs n >= 4"));
     if (s->fast && want_group) {
       auto lt = low_table(ns - (n - 3));
+#ifdef BOTE_DEBUG
+      f.lowtab_n = lt.size();
+#endif
+      // (64 padding entries: a step's lanes read the table past a group's
+      // last row without a clamp; those lanes hold no config)
+      lt.resize(lt.size() + 64, 0u);
       if (s->lowtab.alloc(std::max<size_t>(lt.size(), 1) * 4) != hipSuccess)
         return cleanup(fail(BOTE_E_NOMEM, "hipMalloc group low table"));
       if (!lt.empty() && hipMemcpy(s->lowtab.p, lt.data(), lt.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
         return cleanup(fail(BOTE_E_DEVICE, "upload group low table"));
       f.lowtab = s->lowtab.as<uint32_t>();
-#ifdef BOTE_DEBUG
-      f.lowtab_n = lt.size();
-#endif
       // workgroup size: 256 threads (4 waves).  Larger workgroups (which
       // share the client-quad matrix, so R = 128 fits more waves per CU) were
       // measured slower: R=128 n=6 at 640 threads, 5 waves/SIMD, 369 ms vs

@@ -387,6 +387,14 @@ __device__ __forceinline__ float u64_to_f32(uint64_t x) {
 #ifndef BOTE_BIN_NOFLUSH
 #define BOTE_BIN_NOFLUSH 1
 #endif
+// the step loop's low-table prefetch through a per-lane pointer (VGPRs)
+#ifndef BOTE_LOWTAB_VPTR
+#define BOTE_LOWTAB_VPTR 1
+#endif
+// BIN client loop with lines: quads per unrolled iteration
+#ifndef BOTE_BIN_UB
+#define BOTE_BIN_UB 4
+#endif
 // BN: the base key set with the member-binned client loop (the extended key
 // set's, below); the host picks it for bench-shaped sweeps with >= 96 clients
 // (FastArgs::gbins: R=128 n=6 179.8 -> 168.2 ms; neutral at 64 clients)
@@ -645,14 +653,28 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
       // configs, and the low table's rows are indexed in 32 bits), so its
       // control stays on the scalar unit (there is no 64-bit scalar compare)
       uint32_t left = uni((uint32_t)(cend - r)), lo32 = uni((uint32_t)low);
+#if BOTE_LOWTAB_VPTR
+      // a per-lane pointer into the low table (lane-varying, so it lives in
+      // VGPRs: the table's base is a spilled SGPR pair the step loop would
+      // otherwise reload from VGPR lanes every step); the host pads the table
+      // with 64 rows, so lanes past the group's end read in bounds
+      const uint32_t* ltp = a.lowtab + lo32 + lane;
+      uint32_t lp3 = *ltp;  // prefetched
+#else
       uint32_t lp3 = a.lowtab[lo32 + min(lane, left - 1)];  // prefetched
+#endif
       while (left) {
         const uint32_t len = min(64u, left);
         bool have = lane < len;
         PSTAT(a, 0, true);  // steps
         const uint32_t cur = lp3;
         // prefetch the next step's low part (the load overlaps this step)
+#if BOTE_LOWTAB_VPTR
+        ltp += len;
+        if (left > len) lp3 = *ltp;
+#else
         if (left > len) lp3 = a.lowtab[lo32 + len + min(lane, left - len - 1)];
+#endif
         uint64_t key[MAXOBJ];
         bool ok[MAXOBJ];
 #pragma unroll
@@ -1354,7 +1376,7 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
                   // s2l (squared keys) is flushed to 64 bits every k_flush quads
                   // (4 quads per iteration; 2 without lines, whose 4 sources
                   // per pair of quads would hold 32 VGPRs of reads at 4)
-                  constexpr uint32_t UB = decltype(lines_c)::value ? 4u : 2u;
+                  constexpr uint32_t UB = decltype(lines_c)::value ? (uint32_t)BOTE_BIN_UB : 2u;
                   const uint32_t fU = a.k_flush / UB ? a.k_flush / UB : 1u;
                   uint32_t g = 0, k = 0;
                   if (BOTE_BIN_NOFLUSH && a.k_flush >= nql + UB) {
