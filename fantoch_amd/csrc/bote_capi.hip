@@ -1039,6 +1039,9 @@ int bote_sweep_split(const bote_sweep* s, uint64_t rank_begin, uint64_t rank_end
   return BOTE_OK;
 }
 
+#ifndef BOTE_CHUNK_TAIL
+#define BOTE_CHUNK_TAIL 3  // guided tail rounds of the chunk table (0: equal-cost chunks only)
+#endif
 // The group kernel's work-chunk table for [rb, re): cut from a cached walk
 // and uploaded on `st` once per range (a bench or a shard re-launches the same
 // range).  Null chunks (even rank split in the kernel) off the group kernel.
@@ -1060,7 +1063,10 @@ static int sweep_chunks(bote_sweep* s, uint64_t rb, uint64_t re, hipStream_t st,
     const uint64_t cpw = cpw_env ? std::max(1ul, strtoul(cpw_env, nullptr, 0))
                                  : (uint64_t)chunks_per_wave(re - rb, nwaves, s->fargs.nc, BOTE_CHUNKS_PER_WAVE);
     const uint64_t want = std::min<uint64_t>((uint64_t)nwaves * cpw, (re - rb) / 256 + 1);
-    if (auto w = walk_for(s, rb, re)) c->host = cut_chunks(*w, rb, re, (uint32_t)want);
+    // guided: the launch's last chunks shrink (BOTE_CHUNK_TAIL rounds of one
+    // chunk per wave at 1/2, 1/4, ... of the base size), so the waves finish
+    // within a small chunk of each other instead of a base chunk
+    if (auto w = walk_for(s, rb, re)) c->host = cut_chunks_guided(*w, rb, re, (uint32_t)want, nwaves, BOTE_CHUNK_TAIL);
     if (!c->host.empty()) {
       c->n = (uint32_t)c->host.size() - 1;
       if (c->dev.alloc(c->host.size() * 8) != hipSuccess) return fail(BOTE_E_NOMEM, "hipMalloc work chunks");

@@ -125,6 +125,47 @@ std::shared_ptr<GroupWalk> walk_groups(uint32_t ns, uint32_t n, uint32_t nc, uin
   return w;
 }
 
+// Boundaries of [b, e) at the given cumulative estimated costs (ascending,
+// in wavefront steps; the first chunk starts at b, the last ends at e).
+static std::vector<uint64_t> cut_at(const GroupWalk& w, uint64_t b, uint64_t e, const std::vector<double>& targets);
+
+// The total estimated cost of [b, e) (ceil(len / 64) steps + the group cost
+// per part of a group), the measure the chunk cuts divide.
+static double range_cost(const GroupWalk& w, uint64_t b, uint64_t e) {
+  const size_t i0 = (size_t)(std::upper_bound(w.start.begin(), w.start.end(), b) - w.start.begin()) - 1;
+  const size_t i1 = (size_t)(std::lower_bound(w.start.begin(), w.start.end(), e) - w.start.begin());
+  double total = 0;
+  for (size_t i = i0; i < i1; ++i) {
+    const uint64_t pb = std::max(w.start[i], b), pl = std::min(w.start[i] + w.len[i], e) - pb;
+    total += (double)((pl + 63) / 64) + w.group_cost;
+  }
+  return total;
+}
+
+std::vector<uint64_t> cut_chunks_guided(const GroupWalk& w, uint64_t b, uint64_t e, uint32_t nchunks,
+                                        uint32_t tail_waves, uint32_t levels) {
+  if (e <= b || nchunks == 0 || !w.covers(b, e) || w.start.empty()) return {};
+  // no tail unless every level's chunks fit well inside the range (the tail
+  // holds at most a quarter of the work)
+  if (tail_waves == 0 || levels == 0 || (uint64_t)nchunks < 4ull * tail_waves) return cut_chunks(w, b, e, nchunks);
+  const double total = range_cost(w, b, e), c0 = total / nchunks;
+  double tail = 0;
+  for (uint32_t l = 1; l <= levels; ++l) tail += tail_waves * c0 / (double)(1u << l);
+  const double head = total - tail;
+  const uint32_t nh = (uint32_t)std::max(1.0, std::floor(head / c0 + 0.5));
+  std::vector<double> t;
+  t.reserve(nh + (size_t)levels * tail_waves);
+  for (uint32_t i = 1; i <= nh; ++i) t.push_back(head * i / nh);
+  double at = head;
+  for (uint32_t l = 1; l <= levels; ++l)
+    for (uint32_t k = 0; k < tail_waves; ++k) {
+      at += c0 / (double)(1u << l);
+      t.push_back(at);
+    }
+  t.back() = total;  // (rounding: the last chunk ends at e)
+  return cut_at(w, b, e, t);
+}
+
 std::vector<uint64_t> cut_chunks(const GroupWalk& w, uint64_t b, uint64_t e, uint32_t nchunks) {
   std::vector<uint64_t> out;
   if (e <= b || nchunks == 0 || !w.covers(b, e) || w.start.empty()) return out;
@@ -148,6 +189,36 @@ std::vector<uint64_t> cut_chunks(const GroupWalk& w, uint64_t b, uint64_t e, uin
   size_t i = i0;
   for (uint32_t c = 1; c < nchunks; ++c) {
     const double tgt = total * c / nchunks;
+    uint64_t pb = 0, pl = 0;
+    while (i < i1) {
+      part(i, pb, pl);
+      if (cum + cost(pl) > tgt) break;
+      cum += cost(pl);
+      ++i;
+    }
+    uint64_t bnd = e;
+    if (i < i1) bnd = pb + (uint64_t)((tgt - cum) / cost(pl) * (double)pl);
+    out.push_back(std::max(out.back(), std::min(bnd, e)));
+  }
+  out.push_back(e);
+  return out;
+}
+
+static std::vector<uint64_t> cut_at(const GroupWalk& w, uint64_t b, uint64_t e, const std::vector<double>& targets) {
+  std::vector<uint64_t> out;
+  const size_t i0 = (size_t)(std::upper_bound(w.start.begin(), w.start.end(), b) - w.start.begin()) - 1;
+  const size_t i1 = (size_t)(std::lower_bound(w.start.begin(), w.start.end(), e) - w.start.begin());
+  auto part = [&](size_t i, uint64_t& pb, uint64_t& pl) {
+    pb = std::max(w.start[i], b);
+    pl = std::min(w.start[i] + w.len[i], e) - pb;
+  };
+  auto cost = [&](uint64_t pl) { return (double)((pl + 63) / 64) + w.group_cost; };
+  out.reserve(targets.size() + 1);
+  out.push_back(b);
+  double cum = 0;
+  size_t i = i0;
+  for (size_t c = 0; c + 1 < targets.size(); ++c) {
+    const double tgt = targets[c];
     uint64_t pb = 0, pl = 0;
     while (i < i1) {
       part(i, pb, pl);

@@ -144,6 +144,34 @@ static void check_walk() {
     CHECK(a == direct_chunks(ns, n, nc, b, e, k));
   }
   CHECK(cut_chunks(*w, 5, 5, 4).empty());
+  // the guided table of a full launch (4,096 waves, 32 chunks per wave, 3
+  // tail rounds): ascending, covering [0, total), the base-size chunks then
+  // 3 rounds of 4,096 chunks of 1/2, 1/4, 1/8 of the base size
+  {
+    const uint32_t nw = 4096, cpw = 32;
+    const auto g = cut_chunks_guided(*w, 0, total, nw * cpw, nw, 3);
+    CHECK(g.front() == 0 && g.back() == total);
+    for (size_t i = 1; i < g.size(); ++i) CHECK(g[i - 1] <= g[i]);
+    const size_t nch = g.size() - 1;
+    CHECK(nch > 3 * (size_t)nw && nch < (size_t)nw * cpw + 3 * nw);
+    auto span = [&](size_t i) { return (double)(g[i + 1] - g[i]); };
+    double head = 0, t1 = 0, t3 = 0;
+    for (size_t i = 0; i < nch - 3 * nw; ++i) head += span(i);
+    for (size_t i = nch - 3 * nw; i < nch - 2 * nw; ++i) t1 += span(i);
+    for (size_t i = nch - nw; i < nch; ++i) t3 += span(i);
+    head /= (double)(nch - 3 * nw);
+    t1 /= nw;
+    t3 /= nw;
+    std::printf("guided chunks: %zu, mean ranks per chunk: base %.0f, tail 1/2 %.0f, tail 1/8 %.0f\n", nch, head, t1, t3);
+    CHECK(t1 < 0.7 * head && t3 < 0.25 * head);
+    // no tail: the equal-cost table; too few chunks per wave for a tail: the same
+    CHECK(cut_chunks_guided(*w, 0, total, nw * cpw, 0, 3) == cut_chunks(*w, 0, total, nw * cpw));
+    CHECK(cut_chunks_guided(*w, 0, total, nw * 3, nw, 3) == cut_chunks(*w, 0, total, nw * 3));
+    // a shard's table
+    const auto sg = cut_chunks_guided(*w, sh[3], sh[4], nw * 22, nw, 3);
+    CHECK(sg.front() == sh[3] && sg.back() == sh[4]);
+    for (size_t i = 1; i < sg.size(); ++i) CHECK(sg[i - 1] <= sg[i]);
+  }
   // a walk does not serve a range it does not cover
   auto part = walk_groups(ns, n, nc, 1000, 2000);
   CHECK(part && part->covers(1000, 2000) && !part->covers(999, 2000));

@@ -93,7 +93,18 @@ def test_sweep_keys_vs_fixture(case):
         sw.launch(c["rank_begin"], c["rank_end"])
         r = sw.result()
         got = (r.valid, str(r.digest), [[[str(kk), rr] for kk, rr in lst] for lst in r.tops])
-        assert got == want, f"kernel {k or 'auto'} ({sw.kernel_path()})"
+        if got != want:
+            # (round 5 saw this case fail once in ten suite runs, on the generic
+            # path, with a result block that looked stale: say whether a second
+            # launch of the same sweep agrees, and where the first differs)
+            sw.launch(c["rank_begin"], c["rank_end"])
+            r2 = sw.result()
+            got2 = (r2.valid, str(r2.digest), [[[str(kk), rr] for kk, rr in lst] for lst in r2.tops])
+            bad = [o for o in range(len(want[2])) if got[2][o] != want[2][o]]
+            pytest.fail(f"kernel {k or 'auto'} ({sw.kernel_path()}): counters equal "
+                        f"{got[:2] == want[:2]}, objectives differing {bad}, first records "
+                        f"{[got[2][o][:2] for o in bad[:3]]} vs {[want[2][o][:2] for o in bad[:3]]}; "
+                        f"a second launch equals the fixture: {got2 == want}")
 
 
 def test_r128n6_random_windows_keys_vs_oracle():
