@@ -145,9 +145,11 @@ static double range_cost(const GroupWalk& w, uint64_t b, uint64_t e) {
 std::vector<uint64_t> cut_chunks_guided(const GroupWalk& w, uint64_t b, uint64_t e, uint32_t nchunks,
                                         uint32_t tail_waves, uint32_t levels) {
   if (e <= b || nchunks == 0 || !w.covers(b, e) || w.start.empty()) return {};
-  // no tail unless every level's chunks fit well inside the range (the tail
-  // holds at most a quarter of the work)
-  if (tail_waves == 0 || levels == 0 || (uint64_t)nchunks < 4ull * tail_waves) return cut_chunks(w, b, e, nchunks);
+  // no tail unless the launch has at least 16 base chunks per wave (the tail
+  // holds at most 1/16 of the work; on small shards, 8 chunks per wave, the
+  // extra chunk-start precomputes cost more than the tail saves: r05q, 1/64
+  // of R=64 n=7 0.496 vs 0.481 ms per step)
+  if (tail_waves == 0 || levels == 0 || (uint64_t)nchunks < 16ull * tail_waves) return cut_chunks(w, b, e, nchunks);
   const double total = range_cost(w, b, e), c0 = total / nchunks;
   double tail = 0;
   for (uint32_t l = 1; l <= levels; ++l) tail += tail_waves * c0 / (double)(1u << l);

@@ -51,8 +51,8 @@ std::vector<uint64_t> cut_chunks(const GroupWalk& w, uint64_t b, uint64_t e, uin
 // The work-chunk table of a launch (guided): chunks of the base size
 // (total / nchunks) for most of the range, then `levels` rounds of
 // `tail_waves` chunks each of 1/2, 1/4, ... of it, so that the waves that
-// take the last chunks finish close together.  cut_chunks when the tail
-// would not fit (nchunks < 4 tail_waves) or tail_waves == 0.
+// take the last chunks finish close together.  cut_chunks when the launch
+// is small (nchunks < 16 tail_waves) or tail_waves == 0.
 std::vector<uint64_t> cut_chunks_guided(const GroupWalk& w, uint64_t b, uint64_t e, uint32_t nchunks,
                                         uint32_t tail_waves, uint32_t levels);
 // Work chunks per wavefront for a launch of `ranks` configs on `nwaves`

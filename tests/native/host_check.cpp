@@ -166,7 +166,7 @@ static void check_walk() {
     CHECK(t1 < 0.7 * head && t3 < 0.25 * head);
     // no tail: the equal-cost table; too few chunks per wave for a tail: the same
     CHECK(cut_chunks_guided(*w, 0, total, nw * cpw, 0, 3) == cut_chunks(*w, 0, total, nw * cpw));
-    CHECK(cut_chunks_guided(*w, 0, total, nw * 3, nw, 3) == cut_chunks(*w, 0, total, nw * 3));
+    CHECK(cut_chunks_guided(*w, 0, total, nw * 8, nw, 3) == cut_chunks(*w, 0, total, nw * 8));
     // a shard's table
     const auto sg = cut_chunks_guided(*w, sh[3], sh[4], nw * 22, nw, 3);
     CHECK(sg.front() == sh[3] && sg.back() == sh[4]);
