@@ -365,10 +365,9 @@ __device__ __forceinline__ float u64_to_f32(uint64_t x) {
 // on the PERM kernels, with config 5's objective set compiled in (the
 // default five, then MEAN tt1, MEAN tw2, MEAN fl1: bote.py CONFIG5_OBJECTIVES)
 // The extended key set keeps NT = 3..4 tables of byte planes and sums live
-// through the client loop: its kernels target 3 waves per SIMD (<= 168
-// VGPRs); config 5 (R = 128) is LDS-bound at 3 workgroups per CU anyway.
-// (a 1024-thread bound would cap registers at 128 whatever the wave target:
-// the XK kernels are bounded to 768-thread workgroups, 3 waves per SIMD each)
+// through the client loop: at 4 waves per SIMD (128 VGPRs) part of that state
+// lives in scratch, and still the extra wave per SIMD hides more latency than
+// the scratch traffic costs (config 5: 186 vs 198 ms at 3 waves, 168 VGPRs)
 // (BOTE_GROUP_WAVES_XK, GROUP_XK_MAX_BD = 256 x that: bote_kernels.hpp)
 // client-loop quads per iteration of the base kernels (a build knob)
 #ifndef BOTE_GROUP_UNROLL
@@ -1803,7 +1802,10 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
     // the one-launch merge follows: publish this list's K-th key (a bound on
     // the union's K-th key), then write only the records within the least
     // bound seen so far and a terminator (tk.thr is free now: its key holds
-    // the bound)
+    // the bound).  The terminator/padding is (~0, ~0): a real record may
+    // have key ~0 (a NaN COV key, cov_key) but its rank is < C(R, n) < 2^64
+    // - 1, so the two never match, and a ~0 key is written only when no
+    // bound is known (b == ~0)
     if (tid < a.n_obj) {
       const Rec kth = tk.top[tid * a.K + a.K - 1];
       uint64_t b = ~0ull;

@@ -215,13 +215,14 @@ hipError_t launch_fast(const FastArgs& a, uint32_t n, uint32_t grid, size_t shm,
                        hipEvent_t e1 = nullptr);
 size_t group_smem_bytes(const FastArgs& a, uint32_t n);
 bool group_uses_lines(uint32_t n);  // n <= 7: client lines (FastArgs::gslots) and register lookups
-// the extended key set's group kernels are bounded to this workgroup size (3
-// waves per SIMD at <= 168 VGPRs; bote_group.hip); the capi's eligibility
-// probe and its geometry loop share it
-// the extended key set's kernels: BOTE_GROUP_WAVES_XK waves per SIMD (3:
-// <= 168 VGPRs), so workgroups of at most that many waves per SIMD
+// the extended key set's group kernels target BOTE_GROUP_WAVES_XK waves per
+// SIMD and are bounded to workgroups of that many waves per SIMD
+// (GROUP_XK_MAX_BD); the capi's eligibility probe and its geometry loop share
+// it. 4 (128 VGPRs, 404 B/lane scratch) beats 3 (168 VGPRs, 252 B/lane) on
+// config 5: 186.1 / 185.8 ms vs 198.3 / 197.9 ms kernel, same valid count and
+// digest (profiles/r05r: DESIGN.md §5)
 #ifndef BOTE_GROUP_WAVES_XK
-#define BOTE_GROUP_WAVES_XK 3
+#define BOTE_GROUP_WAVES_XK 4
 #endif
 constexpr uint32_t GROUP_XK_MAX_BD = 256 * BOTE_GROUP_WAVES_XK;
 bool group_supports_keys(uint32_t n, uint32_t bd);  // the extended key set on the group kernel (n = 4..7, bd <= GROUP_XK_MAX_BD)
