@@ -436,7 +436,14 @@ __device__ __forceinline__ void topk_step(const TopkLds& t, int n_obj, uint32_t 
         t.cand[i] = Rec{key[o], rank};
       }
       __syncthreads();
-      if (*t.cnt > 0) topk_merge(t, o, K);
+      // every wave reads the count before any wave adds the next objective's
+      // candidates: without the second barrier a wave that found no
+      // candidate could run ahead into objective o + 1's atomicAdd while a
+      // slower wave still reads the count for objective o, which then enters
+      // the merge alone and merges unwritten candidate slots
+      const int n = *t.cnt;
+      __syncthreads();
+      if (n > 0) topk_merge(t, o, K);
     }
   }
 }

@@ -74,3 +74,26 @@ def test_sweep_topk_vs_fixture(case):
     assert got.valid == c["valid"]
     assert str(got.digest) == c["digest"]
     assert [[[str(k), r] for k, r in lst] for lst in got.tops] == c["tops"]
+
+
+@pytest.mark.parametrize("kernel", ["generic", "fast"])
+def test_block_topk_repeated_launches_vs_fixture(kernel):
+    """The block top-K of the generic and fast kernels (topk_step,
+    bote_device.hpp) under repetition: the same GCP n = 7 sweep launched 12
+    times through one handle, every result equal to the fixture.  Round 5 saw
+    one stale candidate record enter a list once in ten suite runs: a wave
+    that found no candidate for objective o ran ahead into objective o + 1's
+    candidate count while a slower wave still read it for o (fixed by a
+    barrier after the count is read)."""
+    t = json.load(open(os.path.join(G, "topk.json")))
+    c = t["cases"]["gcp_n7"]
+    dp = DevicePlanet(Planet.new())
+    s = np.arange(dp.planet.R, dtype=np.uint32)
+    sw = Sweep(dp, s, s, c["n"], DEFAULT_OBJECTIVES, K=t["K"], ranking=DEFAULT_RANKING, digest=True, kernel=kernel)
+    assert sw.kernel_path() == kernel
+    want = (c["valid"], c["digest"], c["tops"])
+    for i in range(12):
+        sw.launch(c["rank_begin"], c["rank_end"])
+        r = sw.result()
+        got = (r.valid, str(r.digest), [[[str(k), rr] for k, rr in lst] for lst in r.tops])
+        assert got == want, f"launch {i} of the {kernel} kernel differs from tests/golden/topk.json"
