@@ -378,6 +378,9 @@ __device__ __forceinline__ float u64_to_f32(uint64_t x) {
 // half (op_sel picks the high one) instead of v_and / v_bfe + v_lshl_add
 // (profiles/r05e issue rates: v_mad_u32_u16 0.91, v_and 1.62, v_bfe and
 // v_lshl_add 0.95 wave-instructions per CU-clock)
+#ifndef BOTE_BIN_PERMV
+#define BOTE_BIN_PERMV 0  // the bin values' v_perm with every operand in VGPRs (A/B knob)
+#endif
 #ifndef BOTE_BIN_MAD16
 #define BOTE_BIN_MAD16 1
 #endif
@@ -1329,6 +1332,10 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
                 // together (t = w & 0x000F000F), then bin + 256 t.lo16 and
                 // bin + 256 t.hi16 by v_mad_u32_u16 (op_sel selects the half)
                 const uint32_t k256 = 256u;
+                const uint32_t kcnt = 0x01000000u, sel_lo = 0x070C0100u, sel_hi = 0x070C0302u;  // (BOTE_BIN_PERMV)
+                (void)kcnt;
+                (void)sel_lo;
+                (void)sel_hi;
                 auto baddr2 = [&](uint32_t w, uint32_t& lo, uint32_t& hi) {
                   const uint32_t t = w & 0x000F000Fu;
                   asm("v_mad_u32_u16 %0, %1, %2, %3" : "=v"(lo) : "v"(t), "v"(k256), "v"(bin));
@@ -1356,6 +1363,23 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
                   // L2 follows from their sum and the bins (below)
                   s2l = __builtin_amdgcn_udot2(as_us2(L), as_us2(L), s2l, false);
                   s2l = __builtin_amdgcn_udot2(as_us2(H), as_us2(H), s2l, false);
+                  if (BOTE_BIN_MAD16 && BOTE_BIN_PERMV && nv >= 4) {
+                    // (the count constant in a VGPR: the compiler puts it in
+                    // an SGPR operand, A/B knob)
+                    uint32_t aL0, aL1, aH0, aH1;
+                    baddr2(L, aL0, aL1);
+                    baddr2(H, aH0, aH1);
+                    auto pv = [&](uint32_t w, uint32_t sel) {
+                      uint32_t r;
+                      asm("v_perm_b32 %0, %1, %2, %3" : "=v"(r) : "v"(kcnt), "v"(w), "v"(sel));
+                      return r;
+                    };
+                    badd(aL0, pv(L, sel_lo));
+                    badd(aL1, pv(L, sel_hi));
+                    badd(aH0, pv(H, sel_lo));
+                    badd(aH1, pv(H, sel_hi));
+                    return;
+                  }
                   if (BOTE_BIN_MAD16 && nv >= 4) {
                     uint32_t aL0, aL1, aH0, aH1;
                     baddr2(L, aL0, aL1);
