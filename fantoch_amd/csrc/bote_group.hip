@@ -172,6 +172,25 @@ size_t group_smem_bytes(const FastArgs& a, uint32_t n) {
 }
 
 __device__ __forceinline__ uint32_t uni(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
+
+// Late kernel arguments (A/B knob BOTE_LATE_ARGS): a field read through LA()
+// is loaded from the kernarg segment where it is used (a scalar load behind
+// an opaque pointer, so the compiler cannot hoist it out of the step loop)
+// instead of being held in an SGPR across the loop, where the kernel's SGPR
+// pressure spills it to a VGPR lane and every step pays a v_readlane.
+#ifndef BOTE_LATE_ARGS
+#define BOTE_LATE_ARGS 0
+#endif
+__device__ __forceinline__ const __attribute__((address_space(4))) FastArgs* karg_late() {
+  auto p = (const __attribute__((address_space(4))) FastArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(p));
+  return p;
+}
+#if BOTE_LATE_ARGS
+#define LA(f) (karg_late()->f)
+#else
+#define LA(f) (a.f)
+#endif
 __device__ __forceinline__ uint64_t uni64(uint64_t x) {
   return ((uint64_t)uni((uint32_t)(x >> 32)) << 32) | uni((uint32_t)x);
 }
@@ -1072,7 +1091,7 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
           GASSERT(a, bi < (uint32_t)N, 7);  // leader member
           PSTAT(a, 3, amb);  // leader deferred
           if (amb) {
-            if (!a.smin) defer_rank(a, rank);
+            if (!LA(smin)) defer_rank(a, rank);
             have = false;
           }
           if (have) {
@@ -1400,9 +1419,9 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
                   // (4 quads per iteration; 2 without lines, whose 4 sources
                   // per pair of quads would hold 32 VGPRs of reads at 4)
                   constexpr uint32_t UB = decltype(lines_c)::value ? (uint32_t)BOTE_BIN_UB : 2u;
-                  const uint32_t fU = a.k_flush / UB ? a.k_flush / UB : 1u;
+                  const uint32_t kfl = LA(k_flush), fU = kfl / UB ? kfl / UB : 1u;
                   uint32_t g = 0, k = 0;
-                  if (BOTE_BIN_NOFLUSH && a.k_flush >= nql + UB) {
+                  if (BOTE_BIN_NOFLUSH && kfl >= nql + UB) {
                     // one 32-bit sum holds every client's squared key: no
                     // flush test in the loop (a uniform branch)
                     for (; g + UB <= nql; g += UB) {
@@ -1419,7 +1438,7 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
 #pragma unroll
                       for (uint32_t u = 0; u < UB; ++u) quad_bin(Lk[u], Hk[u], 4u);
                     }
-                  } else if (a.k_flush >= UB) {
+                  } else if (kfl >= UB) {
                     for (; g + UB <= nql; g += UB) {
                       uint32_t Lk[UB], Hk[UB];
 #pragma unroll
@@ -1612,7 +1631,7 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
             // V and its f32 value; with FastArgs::v32 (S32 kernels) every
             // V = cnt s2 - s1^2 < cnt s2 fits 32 bits
             auto vmom = [&](const Mom& m, uint64_t& V, float& vf) {
-              if (S32 && a.v32) {
+              if (S32 && LA(v32)) {
                 const uint32_t v = m.cnt * (uint32_t)m.s2 - (uint32_t)m.s1 * (uint32_t)m.s1;
                 V = v;
                 vf = (float)v;
@@ -1642,9 +1661,10 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
                   // fmi >= p1: decided on the integer difference outside
                   // [m1_lo, m1_hi], by the reference's f64 arithmetic inside
                   const int32_t D = (int32_t)((uint32_t)mf.s1 - (uint32_t)ma.s1);
-                  bool mok = D > a.m1_hi;
-                  PSTAT(a, 4 + f - 1, D >= a.m1_lo && D <= a.m1_hi);  // f64 mean test (f = 1, 2)
-                  if (D >= a.m1_lo && D <= a.m1_hi) mok = (mom_mean(mf) - mom_mean(ma)) >= a.p_fmean;
+                  const int32_t m1lo = LA(m1_lo), m1hi = LA(m1_hi);
+                  bool mok = D > m1hi;
+                  PSTAT(a, 4 + f - 1, D >= m1lo && D <= m1hi);  // f64 mean test (f = 1, 2)
+                  if (D >= m1lo && D <= m1hi) mok = (mom_mean(mf) - mom_mean(ma)) >= a.p_fmean;
                   valid = valid && mok;
                   if (N == 11 || N == 13) {
                     const int32_t De = (int32_t)((uint32_t)mom[SLOT_E].s1 - (uint32_t)ma.s1);
@@ -1678,7 +1698,7 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
               }
               PSTAT(a, 8, defer);  // validity deferred
               if (defer) {
-                if (!a.smin) defer_rank(a, rank);
+                if (!LA(smin)) defer_rank(a, rank);
               } else {
                 if (valid) ++valid_cnt;
                 if ((SI || a.want_digest) && !ABLATE(a, 16)) {
@@ -1759,7 +1779,7 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
           }
         }
         // ---- top-K: lock-free screen, exact merge under the block lock
-        if (a.smin) {
+        if (LA(smin)) {
           // sample launch: per objective the least key of this chunk's configs
           const int nobj = XK ? 8 : (DEF ? 5 : a.n_obj);
 #pragma unroll
@@ -1793,7 +1813,7 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
       // (a sample chunk stops at its first group's end: any subset of the
       // range bounds its K-th key, and a sample across many small groups,
       // as at rank 0, cost one precompute each: the launch's slowest wave)
-      if (r >= rend || a.smin) break;
+      if (r >= rend || LA(smin)) break;
       // ---------------- next group: colex successor of the fixed positions
       // (a combination of {3 .. ns-1}; the smallest fixed position is >= 3)
       {

@@ -105,7 +105,7 @@ def main():
     wt0 = next(i + 1 for i, l in enumerate(src) if "void wave_topk(" in l)
     wt1 = next(i + 1 for i, l in enumerate(src) if i + 1 > wt0 and l.startswith("}"))
     # the sample launch's per-chunk minima (a.smin): not run by the sweep launch
-    sm0 = next(i + 1 for i, l in enumerate(src) if "if (a.smin) {" in l)
+    sm0 = next(i + 1 for i, l in enumerate(src) if "if (a.smin) {" in l or "if (LA(smin)) {" in l)
     sm1 = next(i + 1 for i, l in enumerate(src) if i + 1 > sm0 and "} else if (!ABLATE(a, 4)) {" in l)
     regions = [(region_lines(src, m), pst.get(name, 0.0)) for m, name in RARE_REGIONS]
     blk_src = defaultdict(Counter)  # bote_group.hip source lines per block
