@@ -173,24 +173,28 @@ size_t group_smem_bytes(const FastArgs& a, uint32_t n) {
 
 __device__ __forceinline__ uint32_t uni(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
 
-// Late kernel arguments (A/B knob BOTE_LATE_ARGS): a field read through LA()
-// is loaded from the kernarg segment where it is used (a scalar load behind
-// an opaque pointer, so the compiler cannot hoist it out of the step loop)
+// Late kernel arguments (A/B knobs BOTE_LATE_ARGS for the base kernels,
+// BOTE_LATE_ARGS_XK for the extended-key ones): a field read through LA() is
+// loaded from the kernarg segment where it is used (a scalar load behind an
+// opaque pointer, so the compiler cannot hoist it out of the step loop)
 // instead of being held in an SGPR across the loop, where the kernel's SGPR
-// pressure spills it to a VGPR lane and every step pays a v_readlane.
+// pressure spills it to a VGPR lane and every step pays a v_readlane.  At
+// R=64 n=7 it takes the modelled step from 824 to 779 VALU but not the time
+// (13.86 / 13.92 vs 13.85 / 13.87 ms, r05t); config 5: 182.8 / 183.0 vs
+// 185.0 / 185.2 ms.
 #ifndef BOTE_LATE_ARGS
 #define BOTE_LATE_ARGS 0
+#endif
+#ifndef BOTE_LATE_ARGS_XK
+#define BOTE_LATE_ARGS_XK 0
 #endif
 __device__ __forceinline__ const __attribute__((address_space(4))) FastArgs* karg_late() {
   auto p = (const __attribute__((address_space(4))) FastArgs*)__builtin_amdgcn_kernarg_segment_ptr();
   asm volatile("" : "+s"(p));
   return p;
 }
-#if BOTE_LATE_ARGS
-#define LA(f) (karg_late()->f)
-#else
-#define LA(f) (a.f)
-#endif
+// (inside sweep_group_kernel: XK is its template parameter)
+#define LA(f) ((XK ? BOTE_LATE_ARGS_XK : BOTE_LATE_ARGS) ? karg_late()->f : a.f)
 __device__ __forceinline__ uint64_t uni64(uint64_t x) {
   return ((uint64_t)uni((uint32_t)(x >> 32)) << 32) | uni((uint32_t)x);
 }
@@ -398,7 +402,8 @@ __device__ __forceinline__ float u64_to_f32(uint64_t x) {
 // (profiles/r05e issue rates: v_mad_u32_u16 0.91, v_and 1.62, v_bfe and
 // v_lshl_add 0.95 wave-instructions per CU-clock)
 #ifndef BOTE_BIN_PERMV
-#define BOTE_BIN_PERMV 0  // the bin values' v_perm with every operand in VGPRs (A/B knob)
+#define BOTE_BIN_PERMV 1  // the bin values' v_perm with every operand in VGPRs (config 5: 182.7 / 182.9 vs
+                          // 185.0 / 185.2 ms; R=64 n=7 13.84 / 13.86 vs 13.85 / 13.87 ms, r05t)
 #endif
 #ifndef BOTE_BIN_MAD16
 #define BOTE_BIN_MAD16 1
@@ -1383,8 +1388,8 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
                   s2l = __builtin_amdgcn_udot2(as_us2(L), as_us2(L), s2l, false);
                   s2l = __builtin_amdgcn_udot2(as_us2(H), as_us2(H), s2l, false);
                   if (BOTE_BIN_MAD16 && BOTE_BIN_PERMV && nv >= 4) {
-                    // (the count constant in a VGPR: the compiler puts it in
-                    // an SGPR operand, A/B knob)
+                    // the values' v_perm with its constant operands in VGPRs (the
+                    // compiler would pass the count word as an SGPR operand)
                     uint32_t aL0, aL1, aH0, aH1;
                     baddr2(L, aL0, aL1);
                     baddr2(H, aH0, aH1);
