@@ -174,6 +174,17 @@ def test_r128n6_full_keys_group_equals_generic():
         out[k] = (r.valid, r.digest, r.tops)
     assert out["group"] == out["generic"]
     assert out["group"][0] > 0 and all(len(t) == 100 for t in out["group"][2])
+    # every reported record re-derived by the oracle (compute_stats_x +
+    # compute_score on those configs): per objective, the oracle's ordered list
+    # over the 100 reported configs is the device's list, keys bit-exact
+    o = O.OraclePlanet.of(p)
+    rp = (DEFAULT_RANKING.min_mean_fpaxos_improv, DEFAULT_RANKING.min_mean_epaxos_improv,
+          DEFAULT_RANKING.min_fairness_fpaxos_improv, DEFAULT_RANKING.min_mean_decrease)
+    for oi, obj in enumerate(CONFIG5_OBJECTIVES):
+        recs = [(int(k), int(rk)) for k, rk in out["group"][2][oi]]
+        tops, _, _ = o.sweep_ranks(srv, srv, 6, [rk for _, rk in recs], [obj], 100, rp,
+                                   DEFAULT_RANKING.ft_metric.value, threads=8, keys=1)
+        assert [(int(k), int(rk)) for k, rk in tops[0]] == recs, f"objective {oi}"
 
 
 def test_keys_argument_errors():
