@@ -15,7 +15,9 @@
 #            --skip-fixture-check (diagnostics while a fixture is re-pinned)
 #   profile  rocprofv3 kernel trace + stats, then the PMC passes of
 #            scripts/summarize_profile.py, of bench.py on each workload in
-#            PWLS (default WL), to gpurun_out/$TAG/<workload>/
+#            PWLS (default WL), to gpurun_out/$TAG/<workload>/ (PSTEPS steps
+#            after PWARM warm-up steps, default 3 and 1; the summary leaves
+#            the warm-up launches out of its averages)
 #   trace    rocprofv3 kernel trace + stats (no counters) of bench.py for each workload in TWLS
 #   pmc      extra PMC passes: PASSES="ctr ...;ctr ..." over bench.py BENCH_ARGS
 #   shardsteps  scripts/shard_steps.py (a shard's step: wall, kernel, outside) per VARIANTS, + a trace
@@ -77,7 +79,7 @@ step_profile() {
   for wl in ${PWLS:-${WL:-r64n7}}; do
     local P="$O/$wl"
     mkdir -p "$P"
-    local B="python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --workload $wl ${BENCH_ARGS:-}"
+    local B="python3 bench.py --steps ${PSTEPS:-3} --warmup ${PWARM:-1} --no-cpu-baseline --workload $wl ${BENCH_ARGS:-}"
     timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$P/trace" -o run -- $B \
       > "$P/trace.log" 2>&1 || fail "trace $wl" $? "$P/trace.log"
     echo "trace $wl ok"

@@ -3,6 +3,12 @@ profiles/<TAG>_profile.md and update profiles/traffic.json.
 
   python scripts/summarize_profile.py r04d/r64n7 [workload_tag]   (the profile step's output directory)
 
+BOTE_PROFILE_SKIP=N (default: the bench line's own "warmup" count): the first
+N sweep launches of each run are the bench's warm-up (the first one pays the clock ramp and the chunk-table
+build: 14.85 ms vs 13.84-13.99 ms after it in r05u); they are left out of the
+sweep launch's average duration and of the PMC per-dispatch averages (whose
+instruction counts do not depend on it, but the clock estimate does).
+
 Per kernel: calls and average duration (rocprofv3 --kernel-trace --stats), then
 the per-dispatch PMC averages of each counter pass.  HBM traffic per launch of
 the dominant kernel = FETCH_SIZE + WRITE_SIZE (rocprofv3 reports KiB).  The
@@ -27,14 +33,16 @@ def main():
     out = []
     # the profiled library (bench.py's config.lib_build in the runs' own lines):
     # bench.py quotes pmc.json / traffic.json figures only for that build
-    build = None
+    build, warmup = None, None
     for lg in ("trace.log", "pmc1.log"):
         p = os.path.join(src, lg)
         if os.path.exists(p):
             for line in open(p, errors="replace"):
                 if line.startswith("{") and '"lib_build"' in line:
                     try:
-                        build = json.loads(line)["config"]["lib_build"]
+                        d = json.loads(line)
+                        build = d["config"]["lib_build"]
+                        warmup = d.get("warmup")
                     except (ValueError, KeyError):
                         pass
         if build:
@@ -62,13 +70,17 @@ def main():
     if os.path.exists(tr):
         for r in csv.DictReader(open(tr)):
             durs[r["Kernel_Name"]].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+    skip = int(os.environ.get("BOTE_PROFILE_SKIP", warmup if warmup is not None else 1))
     main_avg = {}
     for name, ds in durs.items():
         cut = max(ds) / 4
         big, small = [d for d in ds if d >= cut], [d for d in ds if d < cut]
-        main_avg[name] = sum(big) / len(big)
+        steady = big[skip:] if len(big) > skip else big
+        main_avg[name] = sum(steady) / len(steady)
         if small and "sweep" in name:
-            out.append(f"\n`{name[:70]}`: {len(big)} sweep launches, avg **{main_avg[name] / 1e6:.4f} ms**; "
+            out.append(f"\n`{name[:70]}`: {len(big)} sweep launches, avg **{main_avg[name] / 1e6:.4f} ms** over the "
+                       f"{len(steady)} after the first {len(big) - len(steady)} (warm-up; all {len(big)}: "
+                       f"{sum(big) / len(big) / 1e6:.4f} ms, each: {', '.join(f'{d / 1e6:.3f}' for d in big)}); "
                        f"{len(small)} sample launches (top-K seed), avg {sum(small) / len(small) / 1e6:.4f} ms")
     counters = collections.defaultdict(lambda: collections.defaultdict(float))
     ndisp = collections.defaultdict(set)
@@ -79,8 +91,20 @@ def main():
         for r in rows_i:
             longest[r["Kernel_Name"]] = max(longest[r["Kernel_Name"]],
                                             int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+        # the warm-up sweep launches (the first `skip` big dispatches of each kernel)
+        firsts = collections.defaultdict(list)
+        for r in rows_i:
+            if int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) >= longest[r["Kernel_Name"]] / 4:
+                firsts[r["Kernel_Name"]].append((int(r["Start_Timestamp"]), r["Dispatch_Id"]))
+        warm = set()
+        for k, lst in firsts.items():
+            ids = sorted(set(lst))
+            if len(ids) > skip:
+                warm |= {d for _, d in ids[:skip]}
         for r in rows_i:
             k = r["Kernel_Name"]
+            if r["Dispatch_Id"] in warm:
+                continue
             if int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) < longest[k] / 4:
                 k = k + " [sample launch]"
             counters[k][r["Counter_Name"]] += float(r["Counter_Value"])
