@@ -401,6 +401,9 @@ __device__ __forceinline__ float u64_to_f32(uint64_t x) {
 // half (op_sel picks the high one) instead of v_and / v_bfe + v_lshl_add
 // (profiles/r05e issue rates: v_mad_u32_u16 0.91, v_and 1.62, v_bfe and
 // v_lshl_add 0.95 wave-instructions per CU-clock)
+#ifndef BOTE_BIN_FIRST
+#define BOTE_BIN_FIRST 0  // the binned client loop before the Q phase (A/B knob)
+#endif
 #ifndef BOTE_BIN_PERMV
 #define BOTE_BIN_PERMV 1  // the bin values' v_perm with every operand in VGPRs (config 5: 182.7 / 182.9 vs
                           // 185.0 / 185.2 ms; R=64 n=7 13.84 / 13.86 vs 13.85 / 13.87 ms, r05t)
@@ -766,6 +769,107 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
           uint32_t cv[3];  // RQT column of each variable member
 #pragma unroll
           for (int i = 0; i < 3; ++i) cv[i] = __umul24(rv[i], rstride) + rqt;  // (one v_mad_u32_u24)
+          // BIN_FIRST: the binned client loop runs here, before the Q phase.
+          // It needs only the members' columns and the client line; its
+          // results are the per-lane bins (LDS) and the squared-key sum, so
+          // none of the Q phase, leader choice or every-leader state is live
+          // through it.  The epilogue (below) reads the bins as before.
+          uint64_t L2first = 0;
+          const uint32_t binb = LB + (uint32_t)off[14] + wid * (N * 256) + lane * 4;
+          (void)binb;
+          if constexpr (BIN && BOTE_BIN_FIRST) {
+            const uint32_t f0 = __umul24(rv[0], cstride) + cqt, f1 = __umul24(rv[1], cstride) + cqt,
+                           f2 = __umul24(rv[2], cstride) + cqt;
+            const us2 K1 = {1, 1}, K2 = {2, 2};
+            const uint32_t k256 = 256u, kcnt = 0x01000000u, sel_lo = 0x070C0100u, sel_hi = 0x070C0302u;
+            uint32_t s2f = 0;
+            auto fadd = [&](uint32_t addr, uint32_t v) {
+              __hip_atomic_fetch_add((AS3 uint32_t*)(uintptr_t)addr, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+            };
+            auto fperm = [&](uint32_t w, uint32_t sel) {
+              uint32_t r;
+              asm("v_perm_b32 %0, %1, %2, %3" : "=v"(r) : "v"(kcnt), "v"(w), "v"(sel));
+              return r;
+            };
+            auto fbin = [&](uint32_t L, uint32_t H, uint32_t nv) {
+              if (nv < 4) {  // (the last, partial quad: uniform)
+                L &= nv >= 2 ? ~0u : 0x0000FFFFu;
+                H &= nv == 3 ? 0x0000FFFFu : 0u;
+              }
+              s2f = __builtin_amdgcn_udot2(as_us2(L), as_us2(L), s2f, false);
+              s2f = __builtin_amdgcn_udot2(as_us2(H), as_us2(H), s2f, false);
+              const uint32_t tl = L & 0x000F000Fu, th = H & 0x000F000Fu;
+              uint32_t a0, a1, a2, a3;
+              asm("v_mad_u32_u16 %0, %1, %2, %3" : "=v"(a0) : "v"(tl), "v"(k256), "v"(binb));
+              asm("v_mad_u32_u16 %0, %1, %2, %3 op_sel:[1,0,0,0]" : "=v"(a1) : "v"(tl), "v"(k256), "v"(binb));
+              asm("v_mad_u32_u16 %0, %1, %2, %3" : "=v"(a2) : "v"(th), "v"(k256), "v"(binb));
+              asm("v_mad_u32_u16 %0, %1, %2, %3 op_sel:[1,0,0,0]" : "=v"(a3) : "v"(th), "v"(k256), "v"(binb));
+              fadd(a0, fperm(L, sel_lo));
+              if (nv >= 2) fadd(a1, fperm(L, sel_hi));
+              if (nv >= 3) fadd(a2, fperm(H, sel_lo));
+              if (nv >= 4) fadd(a3, fperm(H, sel_hi));
+            };
+            auto frun = [&](auto lines_c) {
+              constexpr uint32_t UB = decltype(lines_c)::value ? (uint32_t)BOTE_BIN_UB : 2u;
+              const uint32_t nqf = ABLATE(a, 1) ? 0u : nq, kfl = LA(k_flush);
+              uint32_t g = 0;
+              // (unrolled only where UB quads' squared keys fit the 32-bit sum)
+              for (; kfl >= UB && g + UB <= nqf; g += UB) {
+                uint32_t Lk[UB], Hk[UB];
+#pragma unroll
+                for (uint32_t u = 0; u < UB; u += 2) {
+                  const uint32_t g16 = g * 8 + 8 * u;
+                  const uint4 wa = l128(f0 + g16);
+                  us2 lo0, hi0, lo1, hi1;
+                  if constexpr (decltype(lines_c)::value) {
+                    const uint4 wl = l128(ll + g16);
+                    lo0 = pk_min(as_us2(wa.x), as_us2(wl.x));
+                    hi0 = pk_min(as_us2(wa.y), as_us2(wl.y));
+                    lo1 = pk_min(as_us2(wa.z), as_us2(wl.z));
+                    hi1 = pk_min(as_us2(wa.w), as_us2(wl.w));
+                  } else {
+                    const uint4 wb = l128(f1 + g16), wc = l128(f2 + g16), wf = l128(mfl + g16);
+                    lo0 = pk_min(pk_min(as_us2(wa.x), as_us2(wb.x) | K1), pk_min(as_us2(wc.x) | K2, as_us2(wf.x)));
+                    hi0 = pk_min(pk_min(as_us2(wa.y), as_us2(wb.y) | K1), pk_min(as_us2(wc.y) | K2, as_us2(wf.y)));
+                    lo1 = pk_min(pk_min(as_us2(wa.z), as_us2(wb.z) | K1), pk_min(as_us2(wc.z) | K2, as_us2(wf.z)));
+                    hi1 = pk_min(pk_min(as_us2(wa.w), as_us2(wb.w) | K1), pk_min(as_us2(wc.w) | K2, as_us2(wf.w)));
+                  }
+                  Lk[u] = as_u32(lo0);
+                  Hk[u] = as_u32(hi0);
+                  Lk[u + 1] = as_u32(lo1);
+                  Hk[u + 1] = as_u32(hi1);
+                }
+#pragma unroll
+                for (uint32_t u = 0; u < UB; ++u) fbin(Lk[u], Hk[u], 4u);
+                if (kfl < nqf + UB) {  // (uniform) the 32-bit sum could overflow: flush it
+                  L2first += s2f;
+                  s2f = 0;
+                }
+              }
+              // the quads left over, then the partial quad, one at a time
+              for (; g < nqf + (rem && !ABLATE(a, 1) ? 1u : 0u); ++g) {
+                const uint32_t g8 = g * 8, nv = g < nqf ? 4u : rem;
+                const uint2 wa = l64(f0 + g8);
+                us2 lo, hi;
+                if constexpr (decltype(lines_c)::value) {
+                  const uint2 wl = l64(ll + g8);
+                  lo = pk_min(as_us2(wa.x), as_us2(wl.x));
+                  hi = pk_min(as_us2(wa.y), as_us2(wl.y));
+                } else {
+                  const uint2 wb = l64(f1 + g8), wc = l64(f2 + g8), wf = l64(mfl + g8);
+                  lo = pk_min(pk_min(as_us2(wa.x), as_us2(wb.x) | K1), pk_min(as_us2(wc.x) | K2, as_us2(wf.x)));
+                  hi = pk_min(pk_min(as_us2(wa.y), as_us2(wb.y) | K1), pk_min(as_us2(wc.y) | K2, as_us2(wf.y)));
+                }
+                fbin(as_u32(lo), as_u32(hi), nv);
+                L2first += s2f;
+                s2f = 0;
+              }
+              L2first += s2f;
+              s2f = 0;
+            };
+            if (use_lines) frun(BoolC<true>{});
+            else frun(BoolC<false>{});
+          }
           // member m: 0..2 variable, 3.. fixed (config order = ascending positions)
           uint32_t Q2[N], Q3[N];
           uint32_t cS1p = 0, cS1e = 0;  // colocated sums: packed (t0 | t1 << 16), third table
@@ -1098,6 +1202,10 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
           if (amb) {
             if (!LA(smin)) defer_rank(a, rank);
             have = false;
+            if constexpr (BIN && BOTE_BIN_FIRST) {  // the epilogue will not run: re-zero the bins here
+#pragma unroll
+              for (int m = 0; m < N; ++m) s32(binb + 256u * m, 0u);
+            }
           }
           if (have) {
             uint32_t lpos = pv[0], lq2 = Q2[0], lq3 = Q3[0], lreg = rv[0];
@@ -1480,7 +1588,8 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
                   }
                   L2 += s2l;
                 };
-                if (use_lines) clients_bin(BoolC<true>{});
+                if constexpr (BOTE_BIN_FIRST) L2 = L2first;  // (the loop ran before the Q phase)
+                else if (use_lines) clients_bin(BoolC<true>{});
                 else clients_bin(BoolC<false>{});
                 // the bins (re-zeroed for the next config of this lane), in
                 // packed member pairs laid out as the tables' words wp[t][i]
