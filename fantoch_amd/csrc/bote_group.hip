@@ -401,8 +401,14 @@ __device__ __forceinline__ float u64_to_f32(uint64_t x) {
 // half (op_sel picks the high one) instead of v_and / v_bfe + v_lshl_add
 // (profiles/r05e issue rates: v_mad_u32_u16 0.91, v_and 1.62, v_bfe and
 // v_lshl_add 0.95 wave-instructions per CU-clock)
+// the binned client loop before the Q phase (sweep_group_kernel, BIN_FIRST
+// below), per kernel family: config 5's XK kernel 178.1 / 178.6 vs 182.1 /
+// 182.6 ms, the R=64 n=7 kernel 14.07 / 14.05 vs 13.87 / 13.83 ms (r05aa)
 #ifndef BOTE_BIN_FIRST
-#define BOTE_BIN_FIRST 0  // the binned client loop before the Q phase (A/B knob)
+#define BOTE_BIN_FIRST 0
+#endif
+#ifndef BOTE_BIN_FIRST_XK
+#define BOTE_BIN_FIRST_XK 1
 #endif
 #ifndef BOTE_BIN_PERMV
 #define BOTE_BIN_PERMV 1  // the bin values' v_perm with every operand in VGPRs (config 5: 182.7 / 182.9 vs
@@ -449,6 +455,7 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
   constexpr int PF = Pow2<F>::v;                     // fixed-to-fixed row: F values (self = INF), padded
   constexpr bool PERM = GC::PERM;
   constexpr bool BIN = XK || (PERM && (BN || BOTE_GROUP_BIN_ALL));  // the member-binned client loop
+  constexpr bool BIN_FIRST = BIN && (XK ? BOTE_BIN_FIRST_XK : BOTE_BIN_FIRST);  // (its loop before the Q phase)
   static_assert(!XK || (PERM && DEF), "the extended key set runs on the PERM kernels with the default objectives");
   using QT = QTab<N, XK>;
   constexpr int NT = QT::NT;  // leaderless tables (PERM: register byte planes); == NL without XK
@@ -777,7 +784,7 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
           uint64_t L2first = 0;
           const uint32_t binb = LB + (uint32_t)off[14] + wid * (N * 256) + lane * 4;
           (void)binb;
-          if constexpr (BIN && BOTE_BIN_FIRST) {
+          if constexpr (BIN && BIN_FIRST) {
             const uint32_t f0 = __umul24(rv[0], cstride) + cqt, f1 = __umul24(rv[1], cstride) + cqt,
                            f2 = __umul24(rv[2], cstride) + cqt;
             const us2 K1 = {1, 1}, K2 = {2, 2};
@@ -1202,7 +1209,7 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
           if (amb) {
             if (!LA(smin)) defer_rank(a, rank);
             have = false;
-            if constexpr (BIN && BOTE_BIN_FIRST) {  // the epilogue will not run: re-zero the bins here
+            if constexpr (BIN && BIN_FIRST) {  // the epilogue will not run: re-zero the bins here
 #pragma unroll
               for (int m = 0; m < N; ++m) s32(binb + 256u * m, 0u);
             }
@@ -1227,7 +1234,7 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
             auto xslot = [&](uint32_t sl, uint64_t s1, uint64_t s2) { hx = digest_fold(hx, sl, s1, s2); };
             (void)xslot;
             // ---- XK, before the client loop (so that none of it stays live
-            //      through it): FPaxos all leaders (Bote::all_leaders_stats, lib.rs:129-150)
+            //      through it; with BIN_FIRST the loop has run already): FPaxos all leaders (Bote::all_leaders_stats, lib.rs:129-150)
             //      over the Input clients at q = f + 1, members in config
             //      order, from the column sums (closed form, as ff1/ff2); the
             //      digest consumes every one, and slots fl1/fl2 take the best
@@ -1588,7 +1595,7 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
                   }
                   L2 += s2l;
                 };
-                if constexpr (BOTE_BIN_FIRST) L2 = L2first;  // (the loop ran before the Q phase)
+                if constexpr (BIN_FIRST) L2 = L2first;  // (the loop ran before the Q phase)
                 else if (use_lines) clients_bin(BoolC<true>{});
                 else clients_bin(BoolC<false>{});
                 // the bins (re-zeroed for the next config of this lane), in

@@ -73,6 +73,8 @@ MARKERS = [
     ("step head (lowtab, keys init)", "// ---------------- the group's configs, 64 per step"),
     ("client lines build", "// ---- PERM: client lines."),
     ("Q phase (rows, merges)", "uint32_t pv[3], rv[3];"),
+    ("client loop, before the Q phase (BIN_FIRST)", "// BIN_FIRST: the binned client loop runs here"),
+    ("Q phase (rows, merges; after BIN_FIRST)", "// member m: 0..2 variable, 3.. fixed"),
     ("byte planes + colocated sums", "// ---- PERM: byte planes"),
     ("leader choice", "// ---- FPaxos leader (f = 1"),
     ("XK all leaders", "// ---- XK, before the client loop"),
