@@ -199,3 +199,26 @@ def test_keys_argument_errors():
         Sweep(dp, s, s, 3, CONFIG5_OBJECTIVES, keys=1)
     with pytest.raises(_lib.BoteError, match="group kernel"):  # the group kernel needs the default objectives first
         Sweep(dp, s, s, 5, [(_lib.OBJ_MEAN, _lib.SLOT_TT1)], keys=1, kernel="group")
+
+
+@pytest.mark.parametrize("R,n,nc,rb,re", [(64, 6, 61, 3_000_000, 5_000_000), (64, 7, 62, 100_000_000, 101_500_000),
+                                          (128, 6, 127, 4_000_000_000, 4_002_000_000), (64, 5, 33, 0, 7_624_512)])
+def test_keys_group_client_subsets_equal_generic(R, n, nc, rb, re):
+    """The extended key set on the group kernel with client counts that are not
+    a multiple of 4 (the binned loop's partial last quad, before the Q phase on
+    these kernels) and fewer clients than servers: equal to the exact generic
+    kernel (valid count, digest over every slot and leader, 8 top-K lists)."""
+    p = Planet.synthetic(R)
+    dp = DevicePlanet(p)
+    srv = np.arange(R, dtype=np.uint32)
+    cli = np.arange(nc, dtype=np.uint32)[::-1].copy()
+    out = {}
+    for k in ("group", "generic"):
+        sw = Sweep(dp, srv, cli, n, CONFIG5_OBJECTIVES, K=100, ranking=DEFAULT_RANKING, digest=True, kernel=k,
+                   keys=_lib.KEYS_TEMPO_ALL_LEADERS)
+        assert sw.kernel_path() == k
+        sw.launch(rb, min(re, sw.total))
+        r = sw.result()
+        out[k] = (r.valid, r.digest, r.tops)
+    assert out["group"] == out["generic"]
+    assert out["group"][0] > 0
