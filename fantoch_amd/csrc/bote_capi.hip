@@ -131,6 +131,9 @@ struct bote_sweep {
   DBuf top_alt, counters_alt;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   hipEvent_t last0 = nullptr, last1 = nullptr;  // the last launch's kernel events (ev0/ev1 or a timing slot)
+  // recorded after the last work enqueued on the sweep's buffers (a launch's
+  // merge chain, a result copy): destroy waits on it, not on the device
+  hipEvent_t done = nullptr;
   // per-launch kernel timing since the last bote_sweep_timing_reset
   std::vector<std::pair<hipEvent_t, hipEvent_t>> evpool;
   size_t ev_used = 0;
@@ -830,7 +833,12 @@ int bote_sweep_create_keys(const bote_planet* p, const uint32_t* servers, uint32
     // group kernels keep the moments in 32 bits (bote_group.hip S32)
     // (and the FPaxos moments' 24-bit multiplies: column sum + S1 <= 3 nc max < 2^24)
     f.s32 = (uint64_t)std::max(nc, n) * amax * amax < (1ull << 32) && 3ull * nc * maxlat < (1ull << 24) ? 1u : 0u;
-    f.v32 = f.s32 && (uint64_t)std::max(nc, n) * std::max(nc, n) * amax * amax < (1ull << 32) ? 1u : 0u;
+    // and every V = cnt s2 - s1^2 in 32 bits: V = sum over pairs of
+    // (x_i - x_j)^2 <= (cnt / 2)^2 (2 max)^2 = cnt^2 max^2 for values x in
+    // [0, 2 max], so cnt max < 2^16 suffices (the kernels compute V mod 2^32
+    // from 32-bit products: exact when V < 2^32).  Round 5 asked cnt^2 (2 max)^2
+    // < 2^32, which config 5 (128 clients) missed.
+    f.v32 = f.s32 && (uint64_t)std::max(nc, n) * maxlat < (1ull << 16) ? 1u : 0u;
     f.want_score = a.want_score;
     f.p_fmean = a.p_fmean;
     f.p_emean = a.p_emean;
@@ -995,7 +1003,8 @@ int bote_sweep_create_keys(const bote_planet* p, const uint32_t* servers, uint32
     return cleanup(fail(BOTE_E_NOMEM, "hipMalloc overflow fallback workspace"));
   a.out_top = n_obj ? s->top.as<Rec>() : nullptr;
   s->fargs.out_top = a.out_top;
-  if (hipEventCreate(&s->ev0) != hipSuccess || hipEventCreate(&s->ev1) != hipSuccess)
+  if (hipEventCreate(&s->ev0) != hipSuccess || hipEventCreate(&s->ev1) != hipSuccess ||
+      hipEventCreateWithFlags(&s->done, hipEventDisableTiming) != hipSuccess)
     return cleanup(fail(BOTE_E_DEVICE, "hipEventCreate"));
   *out = s;
   return BOTE_OK;
@@ -1184,43 +1193,29 @@ static int launch_generic(bote_sweep* s, uint64_t rb, uint64_t re, hipStream_t s
 
 // The top-K seed of a group launch over [rb, re) (launch_fast_path): sets
 // f.tseed, or leaves it null when the range is too small to sample.
-#ifndef BOTE_SEED_PER_WAVE
-#define BOTE_SEED_PER_WAVE 1  // sample minima per wave (4,096 slots) instead of per chunk (32,768)
-#endif
-#ifndef BOTE_SEED_STEPS
 // sample steps per wave on a full range (r03v A/B: 8 vs 1, kernel -1.6 %, 1/8
 // shard -5 %; r05g: 4 and 8 give the same R=64 n=7 step, 14.15-14.17 vs
 // 14.16-14.25 ms, and 4 halves the sample launch: 0.14 vs 0.18 ms outside the kernel)
-#define BOTE_SEED_STEPS 4
-#endif
-#ifndef BOTE_SEED_SCALE
-#define BOTE_SEED_SCALE 1  // scale the sample steps with the launch's share of the rank space
-#endif
-#ifndef BOTE_SEED_RUN
-#define BOTE_SEED_RUN 1  // consecutive steps per sample chunk (one group precompute per chunk)
-#endif
+constexpr uint32_t SEED_STEPS = 4;
 static int sample_seed(bote_sweep* s, bote::FastArgs& f, uint64_t rb, uint64_t re, hipStream_t st) {
   const uint32_t nwaves = s->fgrid * (s->fargs.gbd / 64);
   const uint32_t base = std::min<uint32_t>(4096, nwaves);
-  // BOTE_SEED_STEPS one-step chunks per wave, disjoint and at most 1/8 of the
+  // SEED_STEPS one-step chunks per wave, disjoint and at most 1/8 of the
   // range.  (Chunks of 8 consecutive steps, 4,096 of them, measured slower:
   // kernel 15.52 vs 15.35 ms, their K least minima are a looser bound, r03x.)
   const uint64_t fit = (re - rb) / (64 * 8);
-  const uint32_t ssteps = BOTE_SEED_RUN;
-  // sample steps per wave: BOTE_SEED_STEPS on a full sweep; a shard's launch
-  // scales them by sqrt(its share of the rank space), rounded up
-  // (BOTE_SEED_SCALE): the sample costs ~ steps, the block merges it saves
+  const uint32_t ssteps = 1;  // one step per sample chunk (one group precompute each)
+  // sample steps per wave: SEED_STEPS on a full sweep; a shard's launch
+  // scales them by sqrt(its share of the rank space), rounded up: the sample
+  // costs ~ steps, the block merges it saves
   // ~ range / steps, so the best count grows as sqrt(range).  r05g, R=64 n=7
   // shards, 8 scaled (8 / 3 / 1 steps) against 8 fixed: 1/8 shard 2.089 vs
   // 2.125 ms per step, 1/64 0.492 vs 0.531 ms
-  uint32_t steps = BOTE_SEED_STEPS;
-  if (BOTE_SEED_SCALE) {
-    const double share = (double)(re - rb) / (double)binom_u64(s->ns, s->n);
-    steps = (uint32_t)std::max(1.0, std::min((double)BOTE_SEED_STEPS,
-                                             std::ceil(BOTE_SEED_STEPS * std::sqrt(share) - 1e-9)));
-  }
+  const double share = (double)(re - rb) / (double)binom_u64(s->ns, s->n);
+  const uint32_t steps =
+      (uint32_t)std::max(1.0, std::min((double)SEED_STEPS, std::ceil(SEED_STEPS * std::sqrt(share) - 1e-9)));
   const uint32_t nsamp = (uint32_t)std::min<uint64_t>(
-      {(uint64_t)base * std::max<uint32_t>(1, steps / BOTE_SEED_RUN), std::max<uint64_t>(base, fit / ssteps), 65536});
+      {(uint64_t)base * std::max<uint32_t>(1, steps), std::max<uint64_t>(base, fit / ssteps), 65536});
   if (nsamp < s->K || re - rb < (uint64_t)nsamp * ssteps * 64 * 8) return BOTE_OK;
   auto key = std::make_pair(rb, re);
   auto it = s->samples.find(key);
@@ -1257,8 +1252,9 @@ static int sample_seed(bote_sweep* s, bote::FastArgs& f, uint64_t rb, uint64_t r
     it = s->samples.emplace(key, std::move(c)).first;
   }
   const bote_sweep::Chunks* c = it->second.get();
-  // slots: one per wave (BOTE_SEED_PER_WAVE) or one per chunk
-  const uint32_t slots = BOTE_SEED_PER_WAVE && nwaves >= s->K ? nwaves : nsamp;
+  // slots: one per wave (K slots at or below a key are K distinct configs: the
+  // waves' chunks are disjoint), or one per chunk on grids of fewer than K waves
+  const uint32_t slots = nwaves >= s->K ? nwaves : nsamp;
   if (s->smin.reserve((size_t)s->n_obj * slots * 8) != hipSuccess || s->tseed.reserve(bote::MAXOBJ * 8) != hipSuccess)
     return fail(BOTE_E_NOMEM, "hipMalloc top-K seed");
   // (per-wave slots: each wave clears its own at the sample launch's start)
@@ -1367,6 +1363,7 @@ int bote_sweep_launch(bote_sweep* s, uint64_t rank_begin, uint64_t rank_end, voi
   hipStream_t st = (hipStream_t)hip_stream;
   int rc = s->fast ? launch_fast_path(s, rank_begin, rank_end, st) : launch_generic(s, rank_begin, rank_end, st, true);
   if (rc) return rc;
+  HIP_TRY(hipEventRecord(s->done, st));
   s->last_rb = rank_begin;
   s->last_re = rank_end;
   s->last_stream = st;
@@ -1397,6 +1394,7 @@ int bote_sweep_result_device(bote_sweep* s, void* dst, void* hip_stream) {
   HIP_TRY(hipSetDevice(s->p->device));
   // (dst: device memory, or pinned host memory: the direct device-to-host copy)
   HIP_TRY(hipMemcpyAsync(dst, s->result.p, s->result_bytes(), hipMemcpyDefault, (hipStream_t)hip_stream));
+  HIP_TRY(hipEventRecord(s->done, (hipStream_t)hip_stream));
   return BOTE_OK;
 }
 
@@ -1495,11 +1493,15 @@ int bote_sweep_destroy(bote_sweep* s) {
   DevGuard dev_guard;  // the caller's current device is restored on return
   if (!s) return BOTE_OK;
   (void)hipSetDevice(s->p ? s->p->device : 0);
-  // work the last launch enqueued may still run (a launch without a result
-  // call): drain the device before its buffers are freed and handed to the
-  // next allocation (the device, not last_stream: the caller's stream may be
-  // gone by now)
-  if (s->launched) (void)hipDeviceSynchronize();
+  // work the last launch or result copy enqueued may still run (a launch
+  // without a result call): wait for it before the buffers are freed and
+  // handed to the next allocation.  An event, not the caller's stream (it may
+  // be gone by now) and not the device (hipDeviceSynchronize would also wait
+  // for other sweeps' and other threads' work: ADVICE r05)
+  if (s->done) {
+    if (s->launched) (void)hipEventSynchronize(s->done);
+    (void)hipEventDestroy(s->done);
+  }
   for (auto& e : s->evpool) {
     (void)hipEventDestroy(e.first);
     (void)hipEventDestroy(e.second);
@@ -1531,6 +1533,10 @@ struct bote_search {
     DBuf local;  // the shard's result block on its own device (remote shards)
     uint64_t b = 0, e = 0;
     int dev = 0;
+    // (remote shards) peer access to the root device is enabled, so the
+    // result block's copy goes device to device over xGMI; false: the
+    // runtime stages hipMemcpyPeerAsync through host memory
+    bool peer_direct = false;
   };
   std::vector<Shard> sh;
   int root = 0;
@@ -1649,6 +1655,22 @@ int bote_search_create(const bote_planet* const* planets, uint32_t n_devices, co
     if (x.dev == h->root) continue;
     if ((e = hipSetDevice(x.dev)) != hipSuccess) return cleanup(hip_fail(e, "hipSetDevice (shard)"));
     if (x.local.alloc(h->nb) != hipSuccess) return cleanup(fail(BOTE_E_NOMEM, "shard result block"));
+    // the shard's device writes its block into the root's memory: enable its
+    // peer access to the root (xGMI), "already enabled" (another handle, or
+    // the caller) counting as success; without peer access the copy is still
+    // correct, staged through the host by the runtime
+    int can = 0;
+    if ((e = hipDeviceCanAccessPeer(&can, x.dev, h->root)) != hipSuccess)
+      return cleanup(hip_fail(e, "hipDeviceCanAccessPeer"));
+    if (can) {
+      e = hipDeviceEnablePeerAccess(h->root, 0);
+      if (e == hipErrorPeerAccessAlreadyEnabled) {
+        (void)hipGetLastError();  // (clear the sticky "already enabled")
+        e = hipSuccess;
+      }
+      if (e != hipSuccess) return cleanup(hip_fail(e, "hipDeviceEnablePeerAccess (shard to root)"));
+      x.peer_direct = true;
+    }
   }
   // the chunk uploads are stream-ordered before the first launch; drain them
   // here so that create returns with the handle idle

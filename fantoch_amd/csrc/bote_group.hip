@@ -53,17 +53,6 @@ constexpr int GROUP_MAX_BD = 1024;
 #define BOTE_GROUP_WAVES_PERM 4
 #endif
 // qtab member planes are 1 << a.gqsh bytes apart (>= gbd * 4, a power of two)
-// BOTE_GROUP_U8 (a build knob, A/B timing): the PERM client loop on one-byte
-// tables (each table relative to its least member latency; a wavefront whose
-// every config spans < 256 takes it, the others the two-byte planes)
-#ifndef BOTE_GROUP_U8
-#define BOTE_GROUP_U8 0
-#endif
-// BOTE_GROUP_BIN_ALL (a build knob, A/B timing): the member-binned client loop
-// of the extended key set on every PERM kernel
-#ifndef BOTE_GROUP_BIN_ALL
-#define BOTE_GROUP_BIN_ALL 0
-#endif
 
 __host__ __device__ constexpr int cmax(int a, int b) { return a > b ? a : b; }
 template <bool B>
@@ -130,7 +119,8 @@ __host__ __device__ inline size_t group_layout(const FastArgs& a, int N, int NLW
   o = (o + 15) & ~(size_t)15;
   off[5] = o; o += (size_t)a.ns * 8;                   // cs2
   off[6] = o; o += (size_t)a.ns * 8;                   // vcol (f64)
-  off[7] = o;  // (binomials stay in global memory: uniform scalar loads, once per group)
+  off[7] = o; o += (size_t)a.ns * 4;                   // vcol32: V as f32 (the screens' leader V)
+  // (binomials stay in global memory: uniform scalar loads, once per group)
   o = (o + 15) & ~(size_t)15;
   off[8] = o; o += (size_t)(a.gbd / 64) * gline_bytes(a, N, KQ);  // per-wave group lines
   o = (o + 15) & ~(size_t)15;
@@ -142,7 +132,7 @@ __host__ __device__ inline size_t group_layout(const FastArgs& a, int N, int NLW
   // extended key set (PERM kernels): per wave, N member bins of 64 lanes' u32
   // (the client loop's binned sums, sweep_group_kernel)
   o = (o + 15) & ~(size_t)15;
-  off[14] = o; o += perm && (a.keys || a.gbins || BOTE_GROUP_BIN_ALL) ? (size_t)(a.gbd / 64) * N * 256 : 0;
+  off[14] = o; o += perm && (a.keys || a.gbins) ? (size_t)(a.gbd / 64) * N * 256 : 0;
   return o;
 }
 
@@ -173,28 +163,6 @@ size_t group_smem_bytes(const FastArgs& a, uint32_t n) {
 
 __device__ __forceinline__ uint32_t uni(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
 
-// Late kernel arguments (A/B knobs BOTE_LATE_ARGS for the base kernels,
-// BOTE_LATE_ARGS_XK for the extended-key ones): a field read through LA() is
-// loaded from the kernarg segment where it is used (a scalar load behind an
-// opaque pointer, so the compiler cannot hoist it out of the step loop)
-// instead of being held in an SGPR across the loop, where the kernel's SGPR
-// pressure spills it to a VGPR lane and every step pays a v_readlane.  At
-// R=64 n=7 it takes the modelled step from 824 to 779 VALU but not the time
-// (13.86 / 13.92 vs 13.85 / 13.87 ms, r05t); config 5: 182.8 / 183.0 vs
-// 185.0 / 185.2 ms.
-#ifndef BOTE_LATE_ARGS
-#define BOTE_LATE_ARGS 0
-#endif
-#ifndef BOTE_LATE_ARGS_XK
-#define BOTE_LATE_ARGS_XK 0
-#endif
-__device__ __forceinline__ const __attribute__((address_space(4))) FastArgs* karg_late() {
-  auto p = (const __attribute__((address_space(4))) FastArgs*)__builtin_amdgcn_kernarg_segment_ptr();
-  asm volatile("" : "+s"(p));
-  return p;
-}
-// (inside sweep_group_kernel: XK is its template parameter)
-#define LA(f) ((XK ? BOTE_LATE_ARGS_XK : BOTE_LATE_ARGS) ? karg_late()->f : a.f)
 __device__ __forceinline__ uint64_t uni64(uint64_t x) {
   return ((uint64_t)uni((uint32_t)(x >> 32)) << 32) | uni((uint32_t)x);
 }
@@ -287,6 +255,38 @@ __device__ __forceinline__ void merge_lists(const T* A, const T* y, T* L) {
   }
 }
 
+// The SCORE objective's screen as one integer compare (DEF kernels: objective
+// 0).  A config's score numerator T = sum over f of (ff.s1 - af.s1) +
+// 30 (e.s1 - af.s1) is an exact integer (|T| < 2^27), and the config can beat
+// the block list's threshold key only if (double)T >= (tscore - 1e-6) nc,
+// tscore the key's score: for a finite bound b that is T >= ceil(b).  The
+// bound is kept in LDS next to the block lock (lock[1]) and recomputed when the
+// threshold moves (the list's K-th record, under the lock: a few times per
+// block), instead of decoding the key and comparing in f64 every step.  It only
+// rises as the threshold falls, so a stale read is a looser screen.
+__device__ __forceinline__ int32_t score_tlo(uint64_t tkey, uint32_t nc) {
+  if (tkey == ~0ull) return INT32_MIN;  // (no threshold yet)
+  const uint64_t ob = ~tkey;
+  const uint64_t bits = (ob >> 63) ? (ob & 0x7FFFFFFFFFFFFFFFull) : ~ob;
+  const double tscore = __longlong_as_double((long long)bits);
+  if (!(tscore == tscore)) return INT32_MIN;  // (a NaN threshold: every config may beat it)
+  const double b = (tscore - 1e-6) * (double)nc;
+  if (b <= -2147483648.0) return INT32_MIN;
+  if (b > 1073741824.0) return 1073741824;  // (above every |T| < 2^27)
+  return (int32_t)ceil(b);
+}
+
+// The COV-af1 objective's screen bound (DEF kernels: objective 3): its key is
+// the bits of V / S^2 as a double (cov_key), so a config may beat the
+// threshold only if V <= key S^2; f32 with a 2^-10 margin over the screen's
+// rounding, +inf with no threshold (the all-ones key), kept in LDS at lock[2]
+// like score_tlo.  A NaN bound lets every config through (always safe: the
+// merge is exact).
+__device__ __forceinline__ float cov_tf32(uint64_t tkey) {
+  if (tkey == ~0ull) return __builtin_inff();
+  return (float)__longlong_as_double((long long)tkey) * (1.0f + 0x1p-10f);
+}
+
 // ------------------------------------------------ wave-level top-K merge --
 // Called by a whole wavefront (uniform branch).  Takes the block's LDS lock,
 // merges every lane record that beats its objective's K-th record (exact
@@ -298,7 +298,7 @@ __device__ __forceinline__ void merge_lists(const T* A, const T* y, T* L) {
 // over them is a chain of scalar reads, not of dependent LDS loads: in the
 // fill phase, 64 candidates per objective, that latency chain held the block's
 // lock for microseconds per merge and was a fixed ~1 ms per launch).
-__device__ __forceinline__ void wave_topk(const TopkLds& t, int* lock, int n_obj, uint32_t K,
+__device__ __forceinline__ void wave_topk(const TopkLds& t, int* lock, uint32_t nc, int n_obj, uint32_t K,
                                           const uint64_t (&key)[MAXOBJ], const bool (&ok)[MAXOBJ], uint64_t rank) {
   const uint32_t lane = threadIdx.x & 63;
   const int KL = (int)K;
@@ -343,7 +343,12 @@ __device__ __forceinline__ void wave_topk(const TopkLds& t, int* lock, int n_obj
     for (int h = 0; h < KP / 64; ++h)
       if ((int)lane + 64 * h < KL) top[lane + 64 * h] = t.tmp[lane + 64 * h];
     wave_sync();
-    if (lane == 0 && rec_lt(top[K - 1], t.thr[o])) t.thr[o] = top[K - 1];
+    if (lane == 0 && rec_lt(top[K - 1], t.thr[o])) {
+      t.thr[o] = top[K - 1];
+      // (the DEF kernels' screens of objectives 0, SCORE, and 3, COV af1)
+      if (o == 0) lock[1] = score_tlo(top[K - 1].key, nc);
+      if (o == 3) lock[2] = __float_as_int(cov_tf32(top[K - 1].key));
+    }
     wave_sync();
   }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
@@ -392,44 +397,24 @@ __device__ __forceinline__ float u64_to_f32(uint64_t x) {
 // lives in scratch, and still the extra wave per SIMD hides more latency than
 // the scratch traffic costs (config 5: 186 vs 198 ms at 3 waves, 168 VGPRs)
 // (BOTE_GROUP_WAVES_XK, GROUP_XK_MAX_BD = 256 x that: bote_kernels.hpp)
-// client-loop quads per iteration of the base kernels (a build knob)
-#ifndef BOTE_GROUP_UNROLL
-#define BOTE_GROUP_UNROLL 4
-#endif
-// BIN client loop: both clients' member tags of a packed word are masked in
-// one v_and (fast class), then each bin address is one v_mad_u32_u16 of a
-// half (op_sel picks the high one) instead of v_and / v_bfe + v_lshl_add
-// (profiles/r05e issue rates: v_mad_u32_u16 0.91, v_and 1.62, v_bfe and
-// v_lshl_add 0.95 wave-instructions per CU-clock)
-// the binned client loop before the Q phase (sweep_group_kernel, BIN_FIRST
-// below), per kernel family: config 5's XK kernel 178.1 / 178.6 vs 182.1 /
-// 182.6 ms, the R=64 n=7 kernel 14.07 / 14.05 vs 13.87 / 13.83 ms (r05aa)
+// client-loop quads per iteration of the register-lookup (PERM) loop
+constexpr uint32_t GROUP_UNROLL = 4;
+// The binned client loop (BIN, below) runs before the Q phase on the XK
+// kernels and after the leader choice on the others (BIN_FIRST): config 5's
+// XK kernel 178.1 / 178.6 vs 182.1 / 182.6 ms with it first, the R=64 n=7
+// kernel 14.07 / 14.05 vs 13.87 / 13.83 ms (r05aa).  The only live -D knob of
+// this file; the decided A/Bs of rounds 4-5 (one-byte tables, late kernel
+// arguments, the binned loop on every PERM kernel, the unrolls) are DESIGN.md
+// history, not code.
 #ifndef BOTE_BIN_FIRST
 #define BOTE_BIN_FIRST 0
 #endif
 #ifndef BOTE_BIN_FIRST_XK
 #define BOTE_BIN_FIRST_XK 1
 #endif
-#ifndef BOTE_BIN_PERMV
-#define BOTE_BIN_PERMV 1  // the bin values' v_perm with every operand in VGPRs (config 5: 182.7 / 182.9 vs
-                          // 185.0 / 185.2 ms; R=64 n=7 13.84 / 13.86 vs 13.85 / 13.87 ms, r05t)
-#endif
-#ifndef BOTE_BIN_MAD16
-#define BOTE_BIN_MAD16 1
-#endif
-// BIN client loop: a loop without the in-loop flush test when one 32-bit sum
-// of squared keys holds every client (k_flush >= the quads)
-#ifndef BOTE_BIN_NOFLUSH
-#define BOTE_BIN_NOFLUSH 1
-#endif
-// the step loop's low-table prefetch through a per-lane pointer (VGPRs)
-#ifndef BOTE_LOWTAB_VPTR
-#define BOTE_LOWTAB_VPTR 1
-#endif
-// BIN client loop with lines: quads per unrolled iteration
-#ifndef BOTE_BIN_UB
-#define BOTE_BIN_UB 4
-#endif
+// binned loop with client lines: quads per unrolled iteration (2 without
+// lines: 4 sources per pair of quads would hold 32 VGPRs of reads at 4)
+constexpr uint32_t BIN_UB = 4;
 // BN: the base key set with the member-binned client loop (the extended key
 // set's, below); the host picks it for bench-shaped sweeps with >= 96 clients
 // (FastArgs::gbins: R=128 n=6 179.8 -> 168.2 ms; neutral at 64 clients)
@@ -454,7 +439,7 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
   constexpr int PV = Pow2<N - 1>::v;                 // variable row: N-1 values, padded
   constexpr int PF = Pow2<F>::v;                     // fixed-to-fixed row: F values (self = INF), padded
   constexpr bool PERM = GC::PERM;
-  constexpr bool BIN = XK || (PERM && (BN || BOTE_GROUP_BIN_ALL));  // the member-binned client loop
+  constexpr bool BIN = XK || (PERM && BN);  // the member-binned client loop
   constexpr bool BIN_FIRST = BIN && (XK ? BOTE_BIN_FIRST_XK : BOTE_BIN_FIRST);  // (its loop before the Q phase)
   static_assert(!XK || (PERM && DEF), "the extended key set runs on the PERM kernels with the default objectives");
   using QT = QTab<N, XK>;
@@ -470,6 +455,7 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
   uint2* lrec = (uint2*)(smem + off[4]);  // per position: .x column sum S1, .y f32 bits of 1 / sqrt(V)
   uint64_t* cs2 = (uint64_t*)(smem + off[5]);
   double* vcol = (double*)(smem + off[6]);
+  float* vcol32 = (float*)(smem + off[7]);
   const uint64_t* binom = a.binom;
   TopkLds tk;
   tk.top = (Rec*)(smem + off[9]);
@@ -499,7 +485,11 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
   // thresholds start at the seed keys (FastArgs::tseed: a bound on each
   // objective's K-th key over the launch range, from the sample launch)
   if (tid < MAXOBJ) tk.thr[tid] = a.tseed && tid < a.n_obj ? Rec{a.tseed[tid], ~0ull} : rec_max();
-  if (tid == 0) *lock = 0;
+  if (tid == 0) {
+    lock[0] = 0;
+    lock[1] = score_tlo(a.tseed && a.n_obj ? a.tseed[0] : ~0ull, a.nc);
+    lock[2] = __float_as_int(cov_tf32(a.tseed && a.n_obj > 3 ? a.tseed[3] : ~0ull));
+  }
   // sample launch with a slot per wave: lane o clears the wave's slot of
   // objective o (no memset before the launch); the same lane's atomicMin
   // per chunk follows it in program order
@@ -522,6 +512,7 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
     cs2[i] = c2;
     const double v = (double)((uint64_t)a.nc * c2 - c1 * c1);  // exact: < 2^53
     vcol[i] = v;
+    vcol32[i] = (float)v;
     // w = 1 / sqrt(V): a member's COV is sqrt(V) / S, so the leader screen
     // maximises S * w with no transcendental per config (+inf: COV 0)
     const float w = v > 0.0 ? (float)(1.0 / sqrt(v)) : __builtin_inff();
@@ -689,28 +680,20 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
       // configs, and the low table's rows are indexed in 32 bits), so its
       // control stays on the scalar unit (there is no 64-bit scalar compare)
       uint32_t left = uni((uint32_t)(cend - r)), lo32 = uni((uint32_t)low);
-#if BOTE_LOWTAB_VPTR
       // a per-lane pointer into the low table (lane-varying, so it lives in
       // VGPRs: the table's base is a spilled SGPR pair the step loop would
       // otherwise reload from VGPR lanes every step); the host pads the table
       // with 64 rows, so lanes past the group's end read in bounds
       const uint32_t* ltp = a.lowtab + lo32 + lane;
       uint32_t lp3 = *ltp;  // prefetched
-#else
-      uint32_t lp3 = a.lowtab[lo32 + min(lane, left - 1)];  // prefetched
-#endif
       while (left) {
         const uint32_t len = min(64u, left);
         bool have = lane < len;
         PSTAT(a, 0, true);  // steps
         const uint32_t cur = lp3;
         // prefetch the next step's low part (the load overlaps this step)
-#if BOTE_LOWTAB_VPTR
         ltp += len;
         if (left > len) lp3 = *ltp;
-#else
-        if (left > len) lp3 = a.lowtab[lo32 + len + min(lane, left - len - 1)];
-#endif
         uint64_t key[MAXOBJ];
         bool ok[MAXOBJ];
 #pragma unroll
@@ -776,106 +759,175 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
           uint32_t cv[3];  // RQT column of each variable member
 #pragma unroll
           for (int i = 0; i < 3; ++i) cv[i] = __umul24(rv[i], rstride) + rqt;  // (one v_mad_u32_u24)
-          // BIN_FIRST: the binned client loop runs here, before the Q phase.
-          // It needs only the members' columns and the client line; its
-          // results are the per-lane bins (LDS) and the squared-key sum, so
-          // none of the Q phase, leader choice or every-leader state is live
-          // through it.  The epilogue (below) reads the bins as before.
-          uint64_t L2first = 0;
+          // ---- BIN: the member-binned client loop, one body for both of its
+          //      places (before the Q phase with BIN_FIRST: it needs only the
+          //      members' columns and the client line, and its results are the
+          //      lane's bins in LDS and one squared-key sum, so none of the Q
+          //      phase, leader choice or every-leader state is live through it;
+          //      else after the leader choice).  Per client one LDS add of
+          //      (key | 1 << 24) into its nearest member's bin (this lane's
+          //      word of member m at binb + 256 m): the bin holds cnt_m (bits
+          //      24..31) and K_m, the sum of keys (latency << 4 | m) of the
+          //      member's clients = 16 D1_m + m cnt_m; the squared keys go to a
+          //      v_dot2 sum (returned).  The epilogue (below) turns the bins
+          //      into every table's sums.
           const uint32_t binb = LB + (uint32_t)off[14] + wid * (N * 256) + lane * 4;
           (void)binb;
-          if constexpr (BIN && BIN_FIRST) {
-            const uint32_t f0 = __umul24(rv[0], cstride) + cqt, f1 = __umul24(rv[1], cstride) + cqt,
-                           f2 = __umul24(rv[2], cstride) + cqt;
+          auto binned_clients = [&](auto lines_c, uint32_t c0, uint32_t c1, uint32_t c2) -> uint64_t {
             const us2 K1 = {1, 1}, K2 = {2, 2};
-            const uint32_t k256 = 256u, kcnt = 0x01000000u, sel_lo = 0x070C0100u, sel_hi = 0x070C0302u;
-            uint32_t s2f = 0;
-            auto fadd = [&](uint32_t addr, uint32_t v) {
+            // each client's nearest member, packed (latency << 4 | member):
+            // the lane's member-0 column against its client line, or against
+            // the other three sources when no line was built; two quads per
+            // ds_read_b128 (g16: a 16-B aligned offset)
+            auto nearest = [&](uint32_t g8, uint32_t& L, uint32_t& H) {
+              const uint2 wa = l64(c0 + g8);
+              us2 lo, hi;
+              if constexpr (decltype(lines_c)::value) {
+                const uint2 wl = l64(ll + g8);
+                lo = pk_min(as_us2(wa.x), as_us2(wl.x));
+                hi = pk_min(as_us2(wa.y), as_us2(wl.y));
+              } else {
+                const uint2 wb = l64(c1 + g8), wc = l64(c2 + g8), wf = l64(mfl + g8);
+                lo = pk_min(pk_min(as_us2(wa.x), as_us2(wb.x) | K1), pk_min(as_us2(wc.x) | K2, as_us2(wf.x)));
+                hi = pk_min(pk_min(as_us2(wa.y), as_us2(wb.y) | K1), pk_min(as_us2(wc.y) | K2, as_us2(wf.y)));
+              }
+              L = as_u32(lo);
+              H = as_u32(hi);
+            };
+            auto nearest2 = [&](uint32_t g16, uint32_t& L0, uint32_t& H0, uint32_t& L1, uint32_t& H1) {
+              const uint4 wa = l128(c0 + g16);
+              us2 lo0, hi0, lo1, hi1;
+              if constexpr (decltype(lines_c)::value) {
+                const uint4 wl = l128(ll + g16);
+                lo0 = pk_min(as_us2(wa.x), as_us2(wl.x));
+                hi0 = pk_min(as_us2(wa.y), as_us2(wl.y));
+                lo1 = pk_min(as_us2(wa.z), as_us2(wl.z));
+                hi1 = pk_min(as_us2(wa.w), as_us2(wl.w));
+              } else {
+                const uint4 wb = l128(c1 + g16), wc = l128(c2 + g16), wf = l128(mfl + g16);
+                lo0 = pk_min(pk_min(as_us2(wa.x), as_us2(wb.x) | K1), pk_min(as_us2(wc.x) | K2, as_us2(wf.x)));
+                hi0 = pk_min(pk_min(as_us2(wa.y), as_us2(wb.y) | K1), pk_min(as_us2(wc.y) | K2, as_us2(wf.y)));
+                lo1 = pk_min(pk_min(as_us2(wa.z), as_us2(wb.z) | K1), pk_min(as_us2(wc.z) | K2, as_us2(wf.z)));
+                hi1 = pk_min(pk_min(as_us2(wa.w), as_us2(wb.w) | K1), pk_min(as_us2(wc.w) | K2, as_us2(wf.w)));
+              }
+              L0 = as_u32(lo0);
+              H0 = as_u32(hi0);
+              L1 = as_u32(lo1);
+              H1 = as_u32(hi1);
+            };
+            uint32_t s2l = 0;
+            uint64_t L2 = 0;
+            auto badd = [&](uint32_t addr, uint32_t v) {
               __hip_atomic_fetch_add((AS3 uint32_t*)(uintptr_t)addr, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
             };
-            auto fperm = [&](uint32_t w, uint32_t sel) {
+            // bin address of a member tag t: binb + (t << 8) in one v_lshl_add
+            auto baddr = [&](uint32_t t) {
+              uint32_t r;
+              asm("v_lshl_add_u32 %0, %1, 8, %2" : "=v"(r) : "v"(t), "v"(binb));
+              return r;
+            };
+            // both bin addresses of a packed pair of keys: the tags masked
+            // together (t = w & 0x000F000F, one v_and, fast class), then
+            // binb + 256 t.lo16 and binb + 256 t.hi16 by v_mad_u32_u16
+            // (op_sel selects the half; profiles/r05e: v_mad_u32_u16 0.91,
+            // v_and 1.62, v_bfe and v_lshl_add 0.95 wave-instructions per
+            // CU-clock)
+            const uint32_t k256 = 256u;
+            auto baddr2 = [&](uint32_t w, uint32_t& lo, uint32_t& hi) {
+              const uint32_t t = w & 0x000F000Fu;
+              asm("v_mad_u32_u16 %0, %1, %2, %3" : "=v"(lo) : "v"(t), "v"(k256), "v"(binb));
+              asm("v_mad_u32_u16 %0, %1, %2, %3 op_sel:[1,0,0,0]" : "=v"(hi) : "v"(t), "v"(k256), "v"(binb));
+            };
+            // a client's bin value (key | 1 << 24) by v_perm, every operand in
+            // VGPRs (the compiler would pass the count word as an SGPR operand:
+            // config 5 182.7 / 182.9 vs 185.0 / 185.2 ms, r05t)
+            const uint32_t kcnt = 0x01000000u, sel_lo = 0x070C0100u, sel_hi = 0x070C0302u;
+            auto bval = [&](uint32_t w, uint32_t sel) {
               uint32_t r;
               asm("v_perm_b32 %0, %1, %2, %3" : "=v"(r) : "v"(kcnt), "v"(w), "v"(sel));
               return r;
             };
-            auto fbin = [&](uint32_t L, uint32_t H, uint32_t nv) {
+            // (the keys of a group of quads are read before any of their bin
+            // adds: the compiler cannot tell the bins from the CQT and lines, so
+            // it keeps program order between LDS reads and adds)
+            auto quad_bin = [&](uint32_t L, uint32_t H, uint32_t nv) {
+#ifdef BOTE_DEBUG
+              GASSERT(a, (L & 15u) < (uint32_t)N && ((L >> 16) & 15u) < (uint32_t)N && (H & 15u) < (uint32_t)N &&
+                             ((H >> 16) & 15u) < (uint32_t)N, 8);
+#endif
               if (nv < 4) {  // (the last, partial quad: uniform)
                 L &= nv >= 2 ? ~0u : 0x0000FFFFu;
                 H &= nv == 3 ? 0x0000FFFFu : 0u;
               }
-              s2f = __builtin_amdgcn_udot2(as_us2(L), as_us2(L), s2f, false);
-              s2f = __builtin_amdgcn_udot2(as_us2(H), as_us2(H), s2f, false);
-              const uint32_t tl = L & 0x000F000Fu, th = H & 0x000F000Fu;
-              uint32_t a0, a1, a2, a3;
-              asm("v_mad_u32_u16 %0, %1, %2, %3" : "=v"(a0) : "v"(tl), "v"(k256), "v"(binb));
-              asm("v_mad_u32_u16 %0, %1, %2, %3 op_sel:[1,0,0,0]" : "=v"(a1) : "v"(tl), "v"(k256), "v"(binb));
-              asm("v_mad_u32_u16 %0, %1, %2, %3" : "=v"(a2) : "v"(th), "v"(k256), "v"(binb));
-              asm("v_mad_u32_u16 %0, %1, %2, %3 op_sel:[1,0,0,0]" : "=v"(a3) : "v"(th), "v"(k256), "v"(binb));
-              fadd(a0, fperm(L, sel_lo));
-              if (nv >= 2) fadd(a1, fperm(L, sel_hi));
-              if (nv >= 3) fadd(a2, fperm(H, sel_lo));
-              if (nv >= 4) fadd(a3, fperm(H, sel_hi));
+              // squared keys (16 lat + m)^2 = 256 lat^2 + 32 lat m + m^2: L2
+              // follows from their sum and the bins (epilogue)
+              s2l = __builtin_amdgcn_udot2(as_us2(L), as_us2(L), s2l, false);
+              s2l = __builtin_amdgcn_udot2(as_us2(H), as_us2(H), s2l, false);
+              if (nv >= 4) {
+                uint32_t aL0, aL1, aH0, aH1;
+                baddr2(L, aL0, aL1);
+                baddr2(H, aH0, aH1);
+                badd(aL0, bval(L, sel_lo));
+                badd(aL1, bval(L, sel_hi));
+                badd(aH0, bval(H, sel_lo));
+                badd(aH1, bval(H, sel_hi));
+                return;
+              }
+              badd(baddr(L & 15u), __builtin_amdgcn_perm(0x01000000u, L, 0x070C0100u));
+              if (nv >= 2) badd(baddr(__builtin_amdgcn_ubfe(L, 16, 4)), __builtin_amdgcn_perm(0x01000000u, L, 0x070C0302u));
+              if (nv >= 3) badd(baddr(H & 15u), __builtin_amdgcn_perm(0x01000000u, H, 0x070C0100u));
             };
-            auto frun = [&](auto lines_c) {
-              constexpr uint32_t UB = decltype(lines_c)::value ? (uint32_t)BOTE_BIN_UB : 2u;
-              const uint32_t nqf = ABLATE(a, 1) ? 0u : nq, kfl = LA(k_flush);
-              uint32_t g = 0;
-              // (unrolled only where UB quads' squared keys fit the 32-bit sum)
-              for (; kfl >= UB && g + UB <= nqf; g += UB) {
+            // s2l (squared keys) is flushed to 64 bits every k_flush quads
+            constexpr uint32_t UB = decltype(lines_c)::value ? BIN_UB : 2u;
+            const uint32_t nql = ABLATE(a, 1) ? 0u : nq;
+            const uint32_t kfl = a.k_flush, fU = kfl / UB ? kfl / UB : 1u;
+            uint32_t g = 0, k = 0;
+            if (kfl >= nql + UB) {
+              // one 32-bit sum holds every client's squared key: no flush test
+              // in the loop (a uniform branch; at R=64 the test cost two VCC
+              // v_cndmask and a 64-bit add per iteration)
+              for (; g + UB <= nql; g += UB) {
                 uint32_t Lk[UB], Hk[UB];
 #pragma unroll
-                for (uint32_t u = 0; u < UB; u += 2) {
-                  const uint32_t g16 = g * 8 + 8 * u;
-                  const uint4 wa = l128(f0 + g16);
-                  us2 lo0, hi0, lo1, hi1;
-                  if constexpr (decltype(lines_c)::value) {
-                    const uint4 wl = l128(ll + g16);
-                    lo0 = pk_min(as_us2(wa.x), as_us2(wl.x));
-                    hi0 = pk_min(as_us2(wa.y), as_us2(wl.y));
-                    lo1 = pk_min(as_us2(wa.z), as_us2(wl.z));
-                    hi1 = pk_min(as_us2(wa.w), as_us2(wl.w));
-                  } else {
-                    const uint4 wb = l128(f1 + g16), wc = l128(f2 + g16), wf = l128(mfl + g16);
-                    lo0 = pk_min(pk_min(as_us2(wa.x), as_us2(wb.x) | K1), pk_min(as_us2(wc.x) | K2, as_us2(wf.x)));
-                    hi0 = pk_min(pk_min(as_us2(wa.y), as_us2(wb.y) | K1), pk_min(as_us2(wc.y) | K2, as_us2(wf.y)));
-                    lo1 = pk_min(pk_min(as_us2(wa.z), as_us2(wb.z) | K1), pk_min(as_us2(wc.z) | K2, as_us2(wf.z)));
-                    hi1 = pk_min(pk_min(as_us2(wa.w), as_us2(wb.w) | K1), pk_min(as_us2(wc.w) | K2, as_us2(wf.w)));
-                  }
-                  Lk[u] = as_u32(lo0);
-                  Hk[u] = as_u32(hi0);
-                  Lk[u + 1] = as_u32(lo1);
-                  Hk[u + 1] = as_u32(hi1);
-                }
+                for (uint32_t u = 0; u < UB; u += 2) nearest2(g * 8 + 8 * u, Lk[u], Hk[u], Lk[u + 1], Hk[u + 1]);
 #pragma unroll
-                for (uint32_t u = 0; u < UB; ++u) fbin(Lk[u], Hk[u], 4u);
-                if (kfl < nqf + UB) {  // (uniform) the 32-bit sum could overflow: flush it
-                  L2first += s2f;
-                  s2f = 0;
+                for (uint32_t u = 0; u < UB; ++u) quad_bin(Lk[u], Hk[u], 4u);
+              }
+            } else if (kfl >= UB) {
+              for (; g + UB <= nql; g += UB) {
+                uint32_t Lk[UB], Hk[UB];
+#pragma unroll
+                for (uint32_t u = 0; u < UB; u += 2) nearest2(g * 8 + 8 * u, Lk[u], Hk[u], Lk[u + 1], Hk[u + 1]);
+#pragma unroll
+                for (uint32_t u = 0; u < UB; ++u) quad_bin(Lk[u], Hk[u], 4u);
+                if (++k == fU) {
+                  L2 += s2l;
+                  s2l = 0;
+                  k = 0;
                 }
               }
-              // the quads left over, then the partial quad, one at a time
-              for (; g < nqf + (rem && !ABLATE(a, 1) ? 1u : 0u); ++g) {
-                const uint32_t g8 = g * 8, nv = g < nqf ? 4u : rem;
-                const uint2 wa = l64(f0 + g8);
-                us2 lo, hi;
-                if constexpr (decltype(lines_c)::value) {
-                  const uint2 wl = l64(ll + g8);
-                  lo = pk_min(as_us2(wa.x), as_us2(wl.x));
-                  hi = pk_min(as_us2(wa.y), as_us2(wl.y));
-                } else {
-                  const uint2 wb = l64(f1 + g8), wc = l64(f2 + g8), wf = l64(mfl + g8);
-                  lo = pk_min(pk_min(as_us2(wa.x), as_us2(wb.x) | K1), pk_min(as_us2(wc.x) | K2, as_us2(wf.x)));
-                  hi = pk_min(pk_min(as_us2(wa.y), as_us2(wb.y) | K1), pk_min(as_us2(wc.y) | K2, as_us2(wf.y)));
-                }
-                fbin(as_u32(lo), as_u32(hi), nv);
-                L2first += s2f;
-                s2f = 0;
-              }
-              L2first += s2f;
-              s2f = 0;
-            };
-            if (use_lines) frun(BoolC<true>{});
-            else frun(BoolC<false>{});
+              L2 += s2l;
+              s2l = 0;
+            }
+            for (; g < nql; ++g) {
+              uint32_t Lk, Hk;
+              nearest(g * 8, Lk, Hk);
+              quad_bin(Lk, Hk, 4u);
+              L2 += s2l;
+              s2l = 0;
+            }
+            if (rem && !ABLATE(a, 1)) {
+              uint32_t Lk, Hk;
+              nearest(nq * 8, Lk, Hk);
+              quad_bin(Lk, Hk, rem);
+            }
+            return L2 + s2l;
+          };
+          uint64_t L2first = 0;
+          if constexpr (BIN && BIN_FIRST) {
+            const uint32_t f0 = __umul24(rv[0], cstride) + cqt, f1 = __umul24(rv[1], cstride) + cqt,
+                           f2 = __umul24(rv[2], cstride) + cqt;
+            L2first = use_lines ? binned_clients(BoolC<true>{}, f0, f1, f2) : binned_clients(BoolC<false>{}, f0, f1, f2);
           }
           // member m: 0..2 variable, 3.. fixed (config order = ascending positions)
           uint32_t Q2[N], Q3[N];
@@ -1090,31 +1142,6 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
           //      QL, high byte in byte m of QH; members 0..3 in .x, 4..6 in
           //      .y) and the colocated sums over the members
           uint2 QL[NT], QH[NT];
-          // U8: one-byte planes of (Q - base) per table, valid when every
-          // member lies within 255 of the table's least (u8ok)
-          constexpr bool U8 = PERM && !BIN && S32 && BOTE_GROUP_U8;
-          uint2 QB[U8 ? NT : 1];
-          uint32_t qbase[U8 ? NT : 1];
-          bool u8ok = true;
-          if constexpr (U8) {
-#pragma unroll
-            for (int t = 0; t < NT; ++t) {
-              const uint32_t w01 = wp[t][0], w2 = wp[t][1], w34 = wp[t][2];
-              const uint32_t w56 = FP >= 2 ? wp[t][FP >= 2 ? 3 : 2] : w34;  // (N < 7: w34 again)
-              const bool hi56 = N >= 7;  // member 6 present (w56's high half)
-              const us2 mn = pk_min(pk_min(as_us2(w01), as_us2(w34)), as_us2(hi56 ? w56 : (w56 | 0xFFFF0000u)));
-              const us2 mx = pk_max(pk_max(as_us2(w01), as_us2(w34)), as_us2(hi56 ? w56 : (w56 & 0xFFFFu)));
-              const uint32_t base = min(min((uint32_t)mn.x, (uint32_t)mn.y), w2 & 0xFFFFu);
-              const uint32_t top = max(max((uint32_t)mx.x, (uint32_t)mx.y), w2 & 0xFFFFu);
-              u8ok = u8ok && top - base < 256u;
-              const uint32_t bb = base | (base << 16);
-              const uint32_t b01 = w01 - bb, b2 = w2 - base, b34 = w34 - bb;
-              const uint32_t b56 = hi56 ? w56 - bb : w56 - base;
-              QB[t].x = __builtin_amdgcn_perm(b2, b01, 0x0C040200u) | (b34 << 24);
-              QB[t].y = __builtin_amdgcn_perm(b56, b34, 0x0C060402u);
-              qbase[t] = base;
-            }
-          }
           if constexpr (PERM) {
 #pragma unroll
             for (int t = 0; t < NT; ++t) {
@@ -1207,7 +1234,7 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
           GASSERT(a, bi < (uint32_t)N, 7);  // leader member
           PSTAT(a, 3, amb);  // leader deferred
           if (amb) {
-            if (!LA(smin)) defer_rank(a, rank);
+            if (!a.smin) defer_rank(a, rank);
             have = false;
             if constexpr (BIN && BIN_FIRST) {  // the epilogue will not run: re-zero the bins here
 #pragma unroll
@@ -1222,8 +1249,9 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
                 lpos = pos_of(l);
                 lq2 = Q2[l];
                 lq3 = Q3[l];
-                lreg = reg_of(l);
+                if constexpr (!SI) lreg = reg_of(l);
               }
+            if constexpr (SI) lreg = lpos;  // (servers in region order: position = region)
             Mom mom[NSLOT];
             // XK: the extended slots and every leader's FPaxos moments are
             // folded into the digest (a linear fold: any order) as they are
@@ -1332,7 +1360,7 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
                   hi1 = pk_min(pk_min(as_us2(wa.w), as_us2(wb.w) | J1), pk_min(as_us2(wc.w) | J2, as_us2(wf.w)));
                 }
               };
-              auto quad_at = [&](auto u8_c, us2 lo, us2 hi, uint32_t mlo, uint32_t mhi) {
+              auto quad_at = [&](us2 lo, us2 hi, uint32_t mlo, uint32_t mhi) {
                 const uint32_t L = as_u32(lo), H = as_u32(hi);
 #ifdef BOTE_DEBUG
                 // every client's nearest-member tag names a member (low 4 bits)
@@ -1348,15 +1376,7 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
                   s2[t] = __builtin_amdgcn_udot2(as_us2(a01), as_us2(a01), s2[t], false);
                   s2[t] = __builtin_amdgcn_udot2(as_us2(a23), as_us2(a23), s2[t], false);
                 };
-                if constexpr (U8 && decltype(u8_c)::value) {
-                  // one-byte planes: the selectors (tag, zero, tag, zero) give
-                  // the two clients' table bytes as a u16 pair in one v_perm
-                  const uint32_t s01 = (L & 0x000F000Fu) | 0x0C000C00u, s23 = (H & 0x000F000Fu) | 0x0C000C00u;
-#pragma unroll
-                  for (int t = 0; t < NT; ++t)
-                    acc1(t, as_us2(__builtin_amdgcn_perm(QB[t].y, QB[t].x, s01)),
-                         as_us2(__builtin_amdgcn_perm(QB[t].y, QB[t].x, s23)));
-                } else if constexpr (PERM) {
+                if constexpr (PERM) {
                   // the 4 clients' member tags as byte selectors, then per
                   // table the low and high bytes of their members' latencies
                   // (v_perm over the byte planes), interleaved into u16 pairs
@@ -1389,16 +1409,16 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
                   }
                 }
               };
-              auto quad = [&](auto lines_c, auto u8_c, uint32_t g8, uint32_t mlo, uint32_t mhi) {
+              auto quad = [&](auto lines_c, uint32_t g8, uint32_t mlo, uint32_t mhi) {
                 us2 lo, hi;
                 nearest(lines_c, g8, lo, hi);
-                quad_at(u8_c, lo, hi, mlo, mhi);
+                quad_at(lo, hi, mlo, mhi);
               };
-              auto quad2 = [&](auto lines_c, auto u8_c, uint32_t g16) {
+              auto quad2 = [&](auto lines_c, uint32_t g16) {
                 us2 lo0, hi0, lo1, hi1;
                 nearest2(lines_c, g16, lo0, hi0, lo1, hi1);
-                quad_at(u8_c, lo0, hi0, ~0u, ~0u);
-                quad_at(u8_c, lo1, hi1, ~0u, ~0u);
+                quad_at(lo0, hi0, ~0u, ~0u);
+                quad_at(lo1, hi1, ~0u, ~0u);
               };
               auto flush = [&]() {
 #pragma unroll
@@ -1414,15 +1434,15 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
               // offset fields); s2 is flushed to 64 bits every s2_flush quads
               // (XK: 2 quads per iteration; its 4 tables' temporaries of 4
               // unrolled quads spill)
-              constexpr uint32_t U = XK ? 2u : (uint32_t)BOTE_GROUP_UNROLL;
+              constexpr uint32_t U = XK ? 2u : GROUP_UNROLL;
               static_assert(U % 2 == 0, "quads are read in 16-B pairs");
-              auto clients = [&](auto lines_c, auto u8_c) {
+              auto clients = [&](auto lines_c) {
                 const uint32_t fU = a.g_flush / U ? a.g_flush / U : 1u;
                 uint32_t g = 0, k = 0;
                 if (a.g_flush >= U) {
                   for (; g + U <= nql; g += U) {
 #pragma unroll
-                    for (uint32_t u = 0; u < U; u += 2) quad2(lines_c, u8_c, g * 8 + 8 * u);  // (g, U even: 16-B aligned)
+                    for (uint32_t u = 0; u < U; u += 2) quad2(lines_c, g * 8 + 8 * u);  // (g, U even: 16-B aligned)
                     if (++k == fU) {
                       flush();
                       k = 0;
@@ -1432,172 +1452,27 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
                 }
                 for (uint32_t g0 = g; g0 < nql; g0 += a.g_flush) {
                   const uint32_t ge = min(nql, g0 + a.g_flush);
-                  for (g = g0; g < ge; ++g) quad(lines_c, u8_c, g * 8, ~0u, ~0u);
+                  for (g = g0; g < ge; ++g) quad(lines_c, g * 8, ~0u, ~0u);
                   flush();
                 }
                 if (rem && !ABLATE(a, 1)) {
-                  quad(lines_c, u8_c, nq * 8, rem >= 2 ? ~0u : 0x0000FFFFu, rem == 3 ? 0x0000FFFFu : 0u);
+                  quad(lines_c, nq * 8, rem >= 2 ? ~0u : 0x0000FFFFu, rem == 3 ? 0x0000FFFFu : 0u);
                   flush();
                 }
               };
               if constexpr (BIN) {
-                // ---- BIN: the clients binned by nearest member, so the loop
-                //      does not depend on the number of tables (4 here).  Per
-                //      client one LDS add of (key | 1 << 24) into its member's
-                //      bin (this lane's word of member m at bin + 256 m): the
-                //      bin holds cnt_m (bits 24..31) and K_m, the sum of keys
-                //      (latency << 4 | m) of the member's clients = 16 D1_m +
-                //      m cnt_m.  Then per table t, exactly,
+                // ---- BIN: the clients binned by nearest member (binned_clients,
+                //      above), so the loop does not depend on the number of
+                //      tables (4 with the extended keys).  Per table t, exactly,
                 //        S1_t = L1 + sum_m cnt_m q_t[m],
                 //        S2_t = L2 + 2 sum_m D1_m q_t[m] + sum_m cnt_m q_t[m]^2
                 //      (L1 = sum of latencies = sum_m D1_m, L2 = sum of squares).
                 //      The host runs this only where the fields cannot overflow
                 //      (nc < 256, nc (16 max + 15) < 2^24; bote_capi.hip).
-                const uint32_t bin = LB + (uint32_t)off[14] + wid * (N * 256) + lane * 4;
-                uint32_t s2l = 0;
-                uint64_t L2 = 0;
-                auto badd = [&](uint32_t addr, uint32_t v) {
-                  __hip_atomic_fetch_add((AS3 uint32_t*)(uintptr_t)addr, v, __ATOMIC_RELAXED,
-                                         __HIP_MEMORY_SCOPE_WAVEFRONT);
-                };
-                // bin address of a client's member tag t: bin + (t << 8) in one
-                // v_lshl_add (the compiler would emit shift, and, add)
-                auto baddr = [&](uint32_t t) {
-                  uint32_t r;
-                  asm("v_lshl_add_u32 %0, %1, 8, %2" : "=v"(r) : "v"(t), "v"(bin));
-                  return r;
-                };
-                // both bin addresses of a packed pair of keys: the tags masked
-                // together (t = w & 0x000F000F), then bin + 256 t.lo16 and
-                // bin + 256 t.hi16 by v_mad_u32_u16 (op_sel selects the half)
-                const uint32_t k256 = 256u;
-                const uint32_t kcnt = 0x01000000u, sel_lo = 0x070C0100u, sel_hi = 0x070C0302u;  // (BOTE_BIN_PERMV)
-                (void)kcnt;
-                (void)sel_lo;
-                (void)sel_hi;
-                auto baddr2 = [&](uint32_t w, uint32_t& lo, uint32_t& hi) {
-                  const uint32_t t = w & 0x000F000Fu;
-                  asm("v_mad_u32_u16 %0, %1, %2, %3" : "=v"(lo) : "v"(t), "v"(k256), "v"(bin));
-                  asm("v_mad_u32_u16 %0, %1, %2, %3 op_sel:[1,0,0,0]" : "=v"(hi) : "v"(t), "v"(k256), "v"(bin));
-                };
-                // (the keys of a group of quads are read before any of their
-                // bin adds: the compiler cannot tell the bins from the CQT and
-                // lines, so it keeps program order between LDS reads and adds)
-                auto quad_keys = [&](auto lines_c, uint32_t g8, uint32_t& L, uint32_t& H) {
-                  us2 lo, hi;
-                  nearest(lines_c, g8, lo, hi);
-                  L = as_u32(lo);
-                  H = as_u32(hi);
-                };
-                auto quad_bin = [&](uint32_t L, uint32_t H, uint32_t nv) {
-#ifdef BOTE_DEBUG
-                  GASSERT(a, (L & 15u) < (uint32_t)N && ((L >> 16) & 15u) < (uint32_t)N && (H & 15u) < (uint32_t)N &&
-                                 ((H >> 16) & 15u) < (uint32_t)N, 8);
-#endif
-                  if (nv < 4) {  // (the last, partial quad: uniform)
-                    L &= nv >= 2 ? ~0u : 0x0000FFFFu;
-                    H &= nv == 3 ? 0x0000FFFFu : 0u;
-                  }
-                  // squared keys (16 lat + m)^2 = 256 lat^2 + 32 lat m + m^2:
-                  // L2 follows from their sum and the bins (below)
-                  s2l = __builtin_amdgcn_udot2(as_us2(L), as_us2(L), s2l, false);
-                  s2l = __builtin_amdgcn_udot2(as_us2(H), as_us2(H), s2l, false);
-                  if (BOTE_BIN_MAD16 && BOTE_BIN_PERMV && nv >= 4) {
-                    // the values' v_perm with its constant operands in VGPRs (the
-                    // compiler would pass the count word as an SGPR operand)
-                    uint32_t aL0, aL1, aH0, aH1;
-                    baddr2(L, aL0, aL1);
-                    baddr2(H, aH0, aH1);
-                    auto pv = [&](uint32_t w, uint32_t sel) {
-                      uint32_t r;
-                      asm("v_perm_b32 %0, %1, %2, %3" : "=v"(r) : "v"(kcnt), "v"(w), "v"(sel));
-                      return r;
-                    };
-                    badd(aL0, pv(L, sel_lo));
-                    badd(aL1, pv(L, sel_hi));
-                    badd(aH0, pv(H, sel_lo));
-                    badd(aH1, pv(H, sel_hi));
-                    return;
-                  }
-                  if (BOTE_BIN_MAD16 && nv >= 4) {
-                    uint32_t aL0, aL1, aH0, aH1;
-                    baddr2(L, aL0, aL1);
-                    baddr2(H, aH0, aH1);
-                    badd(aL0, __builtin_amdgcn_perm(0x01000000u, L, 0x070C0100u));
-                    badd(aL1, __builtin_amdgcn_perm(0x01000000u, L, 0x070C0302u));
-                    badd(aH0, __builtin_amdgcn_perm(0x01000000u, H, 0x070C0100u));
-                    badd(aH1, __builtin_amdgcn_perm(0x01000000u, H, 0x070C0302u));
-                    return;
-                  }
-                  badd(baddr(L & 15u), __builtin_amdgcn_perm(0x01000000u, L, 0x070C0100u));
-                  if (nv >= 2) badd(baddr(__builtin_amdgcn_ubfe(L, 16, 4)), __builtin_amdgcn_perm(0x01000000u, L, 0x070C0302u));
-                  if (nv >= 3) badd(baddr(H & 15u), __builtin_amdgcn_perm(0x01000000u, H, 0x070C0100u));
-                  if (nv >= 4) badd(baddr(__builtin_amdgcn_ubfe(H, 16, 4)), __builtin_amdgcn_perm(0x01000000u, H, 0x070C0302u));
-                };
-                auto clients_bin = [&](auto lines_c) {
-                  // s2l (squared keys) is flushed to 64 bits every k_flush quads
-                  // (4 quads per iteration; 2 without lines, whose 4 sources
-                  // per pair of quads would hold 32 VGPRs of reads at 4)
-                  constexpr uint32_t UB = decltype(lines_c)::value ? (uint32_t)BOTE_BIN_UB : 2u;
-                  const uint32_t kfl = LA(k_flush), fU = kfl / UB ? kfl / UB : 1u;
-                  uint32_t g = 0, k = 0;
-                  if (BOTE_BIN_NOFLUSH && kfl >= nql + UB) {
-                    // one 32-bit sum holds every client's squared key: no
-                    // flush test in the loop (a uniform branch)
-                    for (; g + UB <= nql; g += UB) {
-                      uint32_t Lk[UB], Hk[UB];
-#pragma unroll
-                      for (uint32_t u = 0; u < UB; u += 2) {
-                        us2 lo0, hi0, lo1, hi1;
-                        nearest2(lines_c, g * 8 + 8 * u, lo0, hi0, lo1, hi1);
-                        Lk[u] = as_u32(lo0);
-                        Hk[u] = as_u32(hi0);
-                        Lk[u + 1] = as_u32(lo1);
-                        Hk[u + 1] = as_u32(hi1);
-                      }
-#pragma unroll
-                      for (uint32_t u = 0; u < UB; ++u) quad_bin(Lk[u], Hk[u], 4u);
-                    }
-                  } else if (kfl >= UB) {
-                    for (; g + UB <= nql; g += UB) {
-                      uint32_t Lk[UB], Hk[UB];
-#pragma unroll
-                      for (uint32_t u = 0; u < UB; u += 2) {  // (g, UB even: 16-B aligned pairs of quads)
-                        us2 lo0, hi0, lo1, hi1;
-                        nearest2(lines_c, g * 8 + 8 * u, lo0, hi0, lo1, hi1);
-                        Lk[u] = as_u32(lo0);
-                        Hk[u] = as_u32(hi0);
-                        Lk[u + 1] = as_u32(lo1);
-                        Hk[u + 1] = as_u32(hi1);
-                      }
-#pragma unroll
-                      for (uint32_t u = 0; u < UB; ++u) quad_bin(Lk[u], Hk[u], 4u);
-                      if (++k == fU) {
-                        L2 += s2l;
-                        s2l = 0;
-                        k = 0;
-                      }
-                    }
-                    L2 += s2l;
-                    s2l = 0;
-                  }
-                  for (; g < nql; ++g) {
-                    uint32_t Lk, Hk;
-                    quad_keys(lines_c, g * 8, Lk, Hk);
-                    quad_bin(Lk, Hk, 4u);
-                    L2 += s2l;
-                    s2l = 0;
-                  }
-                  if (rem && !ABLATE(a, 1)) {
-                    uint32_t Lk, Hk;
-                    quad_keys(lines_c, nq * 8, Lk, Hk);
-                    quad_bin(Lk, Hk, rem);
-                  }
-                  L2 += s2l;
-                };
+                uint64_t L2;
                 if constexpr (BIN_FIRST) L2 = L2first;  // (the loop ran before the Q phase)
-                else if (use_lines) clients_bin(BoolC<true>{});
-                else clients_bin(BoolC<false>{});
+                else if (use_lines) L2 = binned_clients(BoolC<true>{}, c0, c1, c2);
+                else L2 = binned_clients(BoolC<false>{}, c0, c1, c2);
                 // the bins (re-zeroed for the next config of this lane), in
                 // packed member pairs laid out as the tables' words wp[t][i]
                 // (members (0, 1), 2, (3, 4), (5, 6); a lone member's high
@@ -1609,8 +1484,8 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
                 uint32_t wv[N], hv[N];  // bin words; (K_m - m cnt_m) >> 4 = D1_m | cnt_m << 20
 #pragma unroll
                 for (int m = 0; m < N; ++m) {
-                  wv[m] = l32(bin + 256u * m);
-                  s32(bin + 256u * m, 0u);
+                  wv[m] = l32(binb + 256u * m);
+                  s32(binb + 256u * m, 0u);
                   hv[m] = (m ? wv[m] - (uint32_t)m * (wv[m] >> 24) : wv[m]) >> 4;
                 }
                 uint32_t cW[NW], dW[NW];  // (cnt_m | cnt_m' << 16), (D1_m | D1_m' << 16)
@@ -1657,24 +1532,8 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
                   if constexpr (S32) S2[t] = (uint32_t)S2[t];  // (< 2^32: FastArgs::s32)
                 }
               } else {
-                // U8: the one-byte loop when every config of the wavefront fits
-                // (a uniform branch), then each table's sums shifted by its base:
-                // S1 = S1' + nc b, S2 = S2' + 2 b S1' + nc b^2
-                if (U8 && __ballot(!u8ok) == 0) {
-                  if (use_lines) clients(BoolC<PERM>{}, BoolC<true>{});
-                  else clients(BoolC<false>{}, BoolC<true>{});
-                  if constexpr (U8) {
-#pragma unroll
-                    for (int t = 0; t < NT; ++t) {
-                      const uint32_t b = qbase[t], s1l = S1[t];
-                      S1[t] = s1l + __umul24(nc, b);
-                      S2[t] = (uint32_t)S2[t] + 2u * b * s1l + __umul24(nc, b) * b;  // (S32: < 2^32)
-                    }
-                  }
-                } else {
-                  if (PERM && use_lines) clients(BoolC<PERM>{}, BoolC<false>{});
-                  else clients(BoolC<false>{}, BoolC<false>{});
-                }
+                if (PERM && use_lines) clients(BoolC<PERM>{});
+                else clients(BoolC<false>{});
               }
               if (ABLATE(a, 1)) {  // timing only: non-degenerate dummy sums
 #pragma unroll
@@ -1741,18 +1600,20 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
               mom[5 + SLOT_AF2] = Mom{cl1[QC::idx_a2], cS2[QC::idx_a2], (uint32_t)N};
               mom[5 + SLOT_E] = Mom{cl1[QC::idx_e], cS2[QC::idx_e], (uint32_t)N};
             }
-            const double vlead = vcol[lpos];
-            const float vlead32 = (float)vlead;
+            // the leader column's V: f32 for the screens (0 exactly when V is),
+            // the exact f64 read only inside a screen's ambiguity band
+            const float vlead32 = vcol32[lpos];
             // af1's exact V (leaderless sums S1 < 2^21, so one 32x32 square),
             // shared by the validity test and the COV-af1 objective screen
             auto mom_v32 = [](const Mom& m) {
               const uint32_t s1 = (uint32_t)m.s1;
               return (uint64_t)m.cnt * m.s2 - (uint64_t)s1 * s1;
             };
-            // V and its f32 value; with FastArgs::v32 (S32 kernels) every
-            // V = cnt s2 - s1^2 < cnt s2 fits 32 bits
+            // V and its f32 value; on the S32 kernels every V = cnt s2 - s1^2
+            // fits 32 bits (the host admits them only with FastArgs::v32), so
+            // 32-bit products give it exactly (mod 2^32)
             auto vmom = [&](const Mom& m, uint64_t& V, float& vf) {
-              if (S32 && LA(v32)) {
+              if constexpr (S32) {
                 const uint32_t v = m.cnt * (uint32_t)m.s2 - (uint32_t)m.s1 * (uint32_t)m.s1;
                 V = v;
                 vf = (float)v;
@@ -1782,7 +1643,7 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
                   // fmi >= p1: decided on the integer difference outside
                   // [m1_lo, m1_hi], by the reference's f64 arithmetic inside
                   const int32_t D = (int32_t)((uint32_t)mf.s1 - (uint32_t)ma.s1);
-                  const int32_t m1lo = LA(m1_lo), m1hi = LA(m1_hi);
+                  const int32_t m1lo = a.m1_lo, m1hi = a.m1_hi;
                   bool mok = D > m1hi;
                   PSTAT(a, 4 + f - 1, D >= m1lo && D <= m1hi);  // f64 mean test (f = 1, 2)
                   if (D >= m1lo && D <= m1hi) mok = (mom_mean(mf) - mom_mean(ma)) >= a.p_fmean;
@@ -1807,8 +1668,8 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
                     uint64_t Va = Va1;
                     float vaf = va1;
                     if (f != 1) vmom(ma, Va, vaf);
-                    if (vlead == 0.0 && Va == 0) continue;  // both COV 0
-                    const int c = cov2_sign(vlead32, (uint32_t)mf.s1, vaf, (uint32_t)ma.s1, [&] { return vlead; },
+                    if (vlead32 == 0.0f && Va == 0) continue;  // both COV 0
+                    const int c = cov2_sign(vlead32, (uint32_t)mf.s1, vaf, (uint32_t)ma.s1, [&] { return vcol[lpos]; },
                                             [&] { return (double)Va; });
                     lt = lt || c < 0;
                     amb_c = amb_c || c == 0;
@@ -1819,7 +1680,7 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
               }
               PSTAT(a, 8, defer);  // validity deferred
               if (defer) {
-                if (!LA(smin)) defer_rank(a, rank);
+                if (!a.smin) defer_rank(a, rank);
               } else {
                 if (valid) ++valid_cnt;
                 if ((SI || a.want_digest) && !ABLATE(a, 16)) {
@@ -1841,23 +1702,16 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
                   key[7] = x_fl1;
                 }
                 if (valid) {
-                  const uint64_t tkey = tk.thr[0].key;
-                  bool maybe = tkey == ~0ull;
-                  if (!maybe) {
-                    const uint64_t ob = ~tkey;
-                    const uint64_t bits = (ob >> 63) ? (ob & 0x7FFFFFFFFFFFFFFFull) : ~ob;
-                    const double tscore = __longlong_as_double((long long)bits);
-                    // (32-bit: every S1 here is below 2^21, so |T| < 2^27)
-                    int32_t T = 0;
+                  // (32-bit: every S1 here is below 2^21, so |T| < 2^27)
+                  int32_t T = 0;
 #pragma unroll
-                    for (int f = 1; f <= 2; ++f) {
-                      if (f > fcap) break;
-                      const int32_t a1 = (int32_t)(uint32_t)mom[f == 1 ? SLOT_AF1 : SLOT_AF2].s1;
-                      T += (int32_t)(uint32_t)mom[f == 1 ? SLOT_FF1 : SLOT_FF2].s1 - a1 +
-                           30 * ((int32_t)(uint32_t)mom[SLOT_E].s1 - a1);
-                    }
-                    maybe = !(tscore == tscore) || (double)T >= (tscore - 1e-6) * (double)nc;
+                  for (int f = 1; f <= 2; ++f) {
+                    if (f > fcap) break;
+                    const int32_t a1 = (int32_t)(uint32_t)mom[f == 1 ? SLOT_AF1 : SLOT_AF2].s1;
+                    T += (int32_t)(uint32_t)mom[f == 1 ? SLOT_FF1 : SLOT_FF2].s1 - a1 +
+                         30 * ((int32_t)(uint32_t)mom[SLOT_E].s1 - a1);
                   }
+                  const bool maybe = T >= *(volatile int*)(lock + 1);  // (score_tlo)
                   PSTAT(a, 9, maybe);  // f64 score
                   if (maybe) {
                     double score = 0.0;
@@ -1878,14 +1732,12 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
                 }
                 {
                   const Mom& m = mom[SLOT_AF1];
-                  const uint64_t tk3 = tk.thr[3].key;
-                  // f32 screen with a 2^-10 margin (conservative: offers a superset)
-                  bool maybe = tk3 == ~0ull;
-                  if (!maybe) {
-                    // V / S^2 <= threshold, cross-multiplied
-                    const float S = (float)(uint32_t)m.s1;
-                    maybe = va1 <= (float)__longlong_as_double((long long)tk3) * (S * S) * (1.0f + 0x1p-10f);
-                  }
+                  // f32 screen with a 2^-10 margin (conservative: offers a
+                  // superset): V / S^2 <= the threshold key's V / S^2,
+                  // cross-multiplied, the threshold's f32 bound from LDS
+                  // (cov_tf32; +inf, or a NaN key: every config passes)
+                  const float S = (float)(uint32_t)m.s1;
+                  const bool maybe = !(va1 > __int_as_float(*(volatile int*)(lock + 2)) * (S * S));
                   PSTAT(a, 10, maybe);  // COV af1 key (f64)
                   if (maybe) {
                     ok[3] = true;
@@ -1894,13 +1746,13 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
                 }
               }
             } else {
-              if (!finish_config<N>(a, mom, vlead, bi, rank, tk.thr, pnc1, pnc2, valid_cnt, digest, key, ok) && !a.smin)
+              if (!finish_config<N>(a, mom, vcol[lpos], bi, rank, tk.thr, pnc1, pnc2, valid_cnt, digest, key, ok) && !a.smin)
                 defer_rank(a, rank);
             }
           }
         }
         // ---- top-K: lock-free screen, exact merge under the block lock
-        if (LA(smin)) {
+        if (a.smin) {
           // sample launch: per objective the least key of this chunk's configs
           const int nobj = XK ? 8 : (DEF ? 5 : a.n_obj);
 #pragma unroll
@@ -1925,16 +1777,15 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
           for (int o = 0; o < MAXOBJ; ++o)
             if (o < nobj) pass = pass || (ok[o] && key[o] <= tk.thr[o].key);
           PSTAT(a, 11, pass);  // block top-K merge
-          if (__ballot(pass)) wave_topk(tk, lock, nobj, a.K, key, ok, rank);
+          if (__ballot(pass)) wave_topk(tk, lock, a.nc, nobj, a.K, key, ok, rank);
         }
         r += len;
-        lo32 += len;
         left -= len;
       }
       // (a sample chunk stops at its first group's end: any subset of the
       // range bounds its K-th key, and a sample across many small groups,
       // as at rank 0, cost one precompute each: the launch's slowest wave)
-      if (r >= rend || LA(smin)) break;
+      if (r >= rend || a.smin) break;
       // ---------------- next group: colex successor of the fixed positions
       // (a combination of {3 .. ns-1}; the smallest fixed position is >= 3)
       {
@@ -2020,7 +1871,8 @@ static hipError_t launch_group_n(const FastArgs& a, uint32_t grid, size_t shm, h
 
 // The instantiation launch_group runs for these arguments (its occupancy
 // decides the persistent grid, so it must be the kernel that runs).
-static bool group_si(const FastArgs& a) { return a.srv_identity && a.want_digest && a.ft_metric == 2 && a.s32; }
+// (S32 kernels also take every V in 32 bits: FastArgs::v32)
+static bool group_si(const FastArgs& a) { return a.srv_identity && a.want_digest && a.ft_metric == 2 && a.s32 && a.v32; }
 
 // the extended key set: PERM kernels (n = 4..7) with the default objectives
 bool group_supports_keys(uint32_t n, uint32_t bd) { return n >= 4 && n <= 7 && group_uses_lines(n) && bd <= GROUP_XK_MAX_BD; }

@@ -790,7 +790,7 @@ hipError_t launch_merge_sel(const Rec* src, uint32_t n_lists, const Rec* alt, ui
 // blocks take statistically similar chunks, so the least of 512 per-block
 // K-th order statistics leaves ~70 of each block's 100 records below it
 // (round 4: ~36 k records per objective, 1.07 ms per step).  So the merge
-// first tightens the bound from the lists' heads (BOTE_MERGE_HEADS):
+// first tightens the bound from the lists' heads:
 //   t = a key with at least K head records at or below it,
 // where the head records (the first WIDE_HEAD of each list) are distinct
 // configs, so the union's K-th key is <= t.  With 512 lists and K = 100 the
@@ -807,9 +807,6 @@ hipError_t launch_merge_sel(const Rec* src, uint32_t n_lists, const Rec* alt, ui
 // WIDE_SORT - K records sorted with the running K least.  The result is the K
 // least of the union whatever the fill (tests/test_merge_model.py restates the
 // procedure and bounds the gathered count).
-#ifndef BOTE_MERGE_HEADS
-#define BOTE_MERGE_HEADS 1  // tighten the bound from the lists' heads (0: round 4's kbound only)
-#endif
 constexpr int WIDE_BD = 1024, WIDE_SORT = 4096, WIDE_LISTS_PER_THREAD = 4, WIDE_HEAD = 2;
 constexpr int WIDE_BINS = 1024, WIDE_WAVES = WIDE_BD / 64, WIDE_SLACK = 32, WIDE_RANK_MAX = 1024;
 // A record with key == ~0 (a NaN COV key) has a real rank < C(R, n) < 2^64 - 1,
@@ -898,6 +895,11 @@ __device__ WideSel wide_select(Each each, uint64_t need, uint32_t* hist, uint32_
         const uint32_t s_lo = s_hi > 10 ? s_hi - 10 : 0, w = s_hi - s_lo;
         hist[tid] = 0;
         __syncthreads();
+        // (shared-count audit, round 6: the adds follow the zeroing barrier;
+        // wave 0 reads the bins only after the barrier below; every thread
+        // reads the pick (ctl[2..4]) after the next one, and the histogram is
+        // zeroed again only after the loop's closing barrier, so no thread can
+        // add into a pass while another still reads the last)
         each([&](uint64_t v, uint64_t) {
           v -= mn;
           if (s_hi >= 64 || (v >> s_hi) == prefix) atomicAdd(&hist[(uint32_t)(v >> s_lo) & ((1u << w) - 1)], 1u);
@@ -937,6 +939,10 @@ __device__ WideSel wide_select(Each each, uint64_t need, uint32_t* hist, uint32_
           each([&](uint64_t v, uint64_t aux) {
             v -= mn;
             if ((v >> s_hi) == prefix) {
+              // (audit: ctl[5] was zeroed by wave 0 before the pick barrier;
+              // the adds precede the barrier below, after which only wave 0
+              // reads the slots, and every path out of here passes a barrier
+              // before ctl is written again)
               const uint32_t k = atomicAdd(&ctl[5], 1u);
               few[k] = v;
               fewa[k] = aux;
@@ -1050,7 +1056,6 @@ __global__ void __launch_bounds__(WIDE_BD) merge_wide_kernel(const Rec* src, uin
   WIDE_T("heads")
   // the bound record (bk, br): the union's K least are at or below it
   uint64_t bk = ~0ull, br = ~0ull;
-#if BOTE_MERGE_HEADS
   {
     // the heads' kept prefix per list (a list's records end at its
     // terminator: what follows it in memory is stale; a key of all ones, a
@@ -1093,9 +1098,7 @@ __global__ void __launch_bounds__(WIDE_BD) merge_wide_kernel(const Rec* src, uin
         if (!rs.none) br = rs.x;
       }
     }
-
   }
-#endif
   const uint64_t kb = min(b0, bk);
   // a record is gathered when it is a real record at or below both bounds
   auto keep = [&](const Rec& r) {
@@ -1200,6 +1203,10 @@ __global__ void __launch_bounds__(WIDE_BD) merge_wide_kernel(const Rec* src, uin
         for (uint32_t c = 0; c < cnt[j]; ++c) d[c] = L[c];
         atomicMax(&ctl[1], off[j] + cnt[j] - w0);
       } else {
+        // (audit: thread 0 resets ctl[0..1] between the two barriers at the
+        // window's start; the atomics follow them, every thread reads
+        // got / next after the barrier below, and the next window's reset
+        // waits for the barrier that opens it)
         atomicMin(&ctl[0], off[j]);
       }
     }
@@ -1218,6 +1225,7 @@ __global__ void __launch_bounds__(WIDE_BD) merge_wide_kernel(const Rec* src, uin
   __syncthreads();
   for (uint32_t i = tid; i < (uint32_t)KP; i += WIDE_BD) out[i] = i < have && i < KK ? buf[i] : rec_max();
 }
+#undef WIDE_T
 
 hipError_t launch_merge_wide(const Rec* src, uint32_t n_lists, const Rec* alt, uint32_t alt_lists, uint64_t list_stride,
                              const unsigned long long* sel, uint64_t cap, const unsigned long long* kbound, Rec* dst,
@@ -1342,6 +1350,10 @@ __global__ void __launch_bounds__(1024) seed_kernel(const uint64_t* smin, uint32
     __syncthreads();
     const uint64_t prefix = sel[0];
     const int sh = 8 * pass;
+    // (audit: the bins are zeroed before the barrier above; wave 0 reads
+    // them after the barrier below and publishes sel[] before the next one;
+    // every thread reads sel[] after it, and the next pass zeroes the bins
+    // only after that barrier, so no add lands in a pass still being read)
     auto count = [&](uint64_t v) {
       if (pass == 7 || (v >> (sh + 8)) == prefix) atomicAdd(&hist[(v >> sh) & 0xFFu], 1u);
     };
@@ -1388,6 +1400,9 @@ __global__ void __launch_bounds__(1024) seed_kernel(const uint64_t* smin, uint32
     if (pass > 0 && sel[2] <= 64) {  // (block-uniform) a small bin: one wave ranks its keys
       const uint64_t pfx = sel[0];
       const int shb = 8 * pass;
+      // (audit: nfew is zeroed by thread 0 before the pick barrier; the
+      // adds follow it and wave 0 reads nfew after the barrier below, then
+      // the block returns: nfew is never added to again in this launch)
       auto push = [&](uint64_t v) {
         if ((v >> shb) == pfx) few[atomicAdd(&nfew, 1u)] = v;
       };

@@ -25,9 +25,6 @@
 // by integer / f64-margin decisions; digest; block top-K.
 #include "bote_fast.hpp"
 
-#ifndef BOTE_QROW_BARRIER
-#define BOTE_QROW_BARRIER 1
-#endif
 
 namespace bote {
 
@@ -362,11 +359,9 @@ __global__ void __launch_bounds__(FAST_BD, 4) sweep_fast_kernel(FastArgs a) {
           }
           *(uint32_t*)(smem + qlane + ((uint32_t)j << QSH)) = ql[0] | (NL >= 2 ? ql[NL >= 2 ? 1 : 0] << 16 : 0u);
           if (NL == 3) *(uint32_t*)(smem + qlane + ((uint32_t)(N + j) << QSH)) = ql[NL - 1];
-#if BOTE_QROW_BARRIER
           // one member row at a time: keeps the row's reads and sort network
           // from being interleaved with the next rows (register pressure)
           __builtin_amdgcn_sched_barrier(0);
-#endif
         }
         // ---- FPaxos leader (f = 1, q = 2, min COV, first in config order)
         uint32_t bi = 0;

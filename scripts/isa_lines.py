@@ -72,9 +72,12 @@ MARKERS = [
     ("group precompute", "// ---------------- per-group, wave-uniform precompute"),
     ("step head (lowtab, keys init)", "// ---------------- the group's configs, 64 per step"),
     ("client lines build", "// ---- PERM: client lines."),
-    ("Q phase (rows, merges)", "uint32_t pv[3], rv[3];"),
-    ("client loop, before the Q phase (BIN_FIRST)", "// BIN_FIRST: the binned client loop runs here"),
-    ("Q phase (rows, merges; after BIN_FIRST)", "// member m: 0..2 variable, 3.. fixed"),
+    ("step members (unpack)", "uint32_t pv[3], rv[3];"),
+    # the member-binned client loop's one body (a lambda: its instructions
+    # carry these lines wherever it runs, before the Q phase on the XK
+    # kernels, after the leader choice on the R=64 kernel)
+    ("client loop (binned body)", "// ---- BIN: the member-binned client loop, one body"),
+    ("Q phase (rows, merges)", "// member m: 0..2 variable, 3.. fixed"),
     ("byte planes + colocated sums", "// ---- PERM: byte planes"),
     ("leader choice", "// ---- FPaxos leader (f = 1"),
     ("XK all leaders", "// ---- XK, before the client loop"),
