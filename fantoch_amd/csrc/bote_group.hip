@@ -133,12 +133,18 @@ __host__ __device__ inline size_t group_layout(const FastArgs& a, int N, int NLW
   // (the client loop's binned sums, sweep_group_kernel)
   o = (o + 15) & ~(size_t)15;
   off[14] = o; o += perm && (a.keys || a.gbins) ? (size_t)(a.gbd / 64) * N * 256 : 0;
+  // per thread, its running digest (u64): an LDS add per step instead of a
+  // 64-bit accumulator held in registers across the step loop, which the
+  // register-bound kernels spilled to scratch and reloaded, added and stored
+  // back every step (config 5: the bulk of its scratch write traffic)
+  o = (o + 15) & ~(size_t)15;
+  off[15] = o; o += (size_t)a.gbd * 8;
   return o;
 }
 
 template <int N>
 static size_t group_smem_n(const FastArgs& a) {
-  size_t off[15];
+  size_t off[16];
   return group_layout(a, N, QCfg<N>::NL <= 2 ? 1 : 2, GCfg<N>::KQ, GCfg<N>::PERM, off);
 }
 
@@ -445,7 +451,7 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
   using QT = QTab<N, XK>;
   constexpr int NT = QT::NT;  // leaderless tables (PERM: register byte planes); == NL without XK
   extern __shared__ __align__(16) unsigned char smem[];
-  size_t off[15];
+  size_t off[16];
   group_layout(a, N, NLW, KQ, PERM, off);
   const uint32_t LB = lds_base(smem);
   const uint32_t qtab = LB + (uint32_t)off[0];
@@ -498,6 +504,7 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
   // BIN: the member bins start at zero (each lane re-zeroes its own after use)
   if constexpr (BIN)
     for (uint32_t i = tid; i < (BD >> 6) * N * 64; i += BD) ((uint32_t*)(smem + off[14]))[i] = 0;
+  ((uint64_t*)(smem + off[15]))[tid] = 0;  // this thread's digest
   __syncthreads();
   const uint32_t cstride = a.cq_stride * 8;  // bytes per CQT column
   const uint32_t rstride = a.rq_stride * 8;
@@ -533,7 +540,14 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
   const uint32_t fS1 = upk + FP * KQ * 4;                                  // fixed column sums
   const uint32_t fVf = fS1 + F * 4;                                        // fixed column 1 / sqrt(V) (f32)
   const double pnc1 = a.p_fmean * (double)nc, pnc2 = a.p_emean * (double)nc;
-  uint64_t valid_cnt = 0, digest = 0;
+  // the wave's valid-config count (uniform: a popcount of the valid lanes per
+  // step, scalar adds) and each lane's running digest in LDS (off[15]):
+  // neither holds vector registers across the step loop
+  uint64_t valid_cnt = 0;
+  const uint32_t dslot = LB + (uint32_t)off[15] + tid * 8;
+  auto digest_add = [&](uint64_t d) {
+    __hip_atomic_fetch_add((AS3 uint64_t*)(uintptr_t)dslot, d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+  };
 
   // Work: either this wave's equal share of [rb, re), or (nwchunks > 0)
   // chunks of equal estimated cost taken from a ticket counter until none is
@@ -696,6 +710,7 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
         if (left > len) lp3 = *ltp;
         uint64_t key[MAXOBJ];
         bool ok[MAXOBJ];
+        bool vflag = false;  // this lane's config is valid (counted by a ballot where the wave has reconverged)
 #pragma unroll
         for (int o = 0; o < MAXOBJ; ++o) {
           key[o] = 0;
@@ -1682,12 +1697,12 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
               if (defer) {
                 if (!a.smin) defer_rank(a, rank);
               } else {
-                if (valid) ++valid_cnt;
+                vflag = valid;
                 if ((SI || a.want_digest) && !ABLATE(a, 16)) {
                   uint32_t h = hx;  // (0 without XK)
 #pragma unroll
                   for (int sl = 0; sl < NSLOT; ++sl) h = digest_fold(h, sl, mom[sl].s1, mom[sl].s2);
-                  digest += digest_final(rank, bi, h);
+                  digest_add(digest_final(rank, bi, h));
                 }
                 // ---- default objectives: 0 SCORE, 1 MEAN af1, 2 MEAN ff1, 3 COV af1, 4 MEAN e
                 if (ABLATE(a, 2048)) valid = false;
@@ -1746,11 +1761,15 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
                 }
               }
             } else {
-              if (!finish_config<N>(a, mom, vcol[lpos], bi, rank, tk.thr, pnc1, pnc2, valid_cnt, digest, key, ok) && !a.smin)
+              uint64_t vc = 0, dg = 0;  // (this config's: finish_config adds to them)
+              if (!finish_config<N>(a, mom, vcol[lpos], bi, rank, tk.thr, pnc1, pnc2, vc, dg, key, ok) && !a.smin)
                 defer_rank(a, rank);
+              vflag = vc != 0;
+              if (dg) digest_add(dg);
             }
           }
         }
+        valid_cnt += (uint64_t)__popcll(__ballot(vflag));  // (every lane active here: a uniform count)
         // ---- top-K: lock-free screen, exact merge under the block lock
         if (a.smin) {
           // sample launch: per objective the least key of this chunk's configs
@@ -1765,8 +1784,15 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
                                  (uint32_t)__shfl_xor((int)(uint32_t)v, d);
               v = w < v ? w : v;
             }
+            uint32_t ch = chunk;
+            // (an opaque copy: the compiler hoisted these 8 slot addresses out
+            // of the step loop into the chunk head, where the register-bound
+            // XK kernel spilled them -- 4 KB of scratch writes per chunk of the
+            // sweep launch, which never takes this branch: most of config 5's
+            // 7.5e8 B of WRITE_SIZE per launch, r06d)
+            asm volatile("" : "+s"(ch));
             const size_t slot = a.smin_wave ? (size_t)o * gridDim.x * WPB + (size_t)blockIdx.x * WPB + wid
-                                            : (size_t)o * a.nwchunks + chunk;
+                                            : (size_t)o * a.nwchunks + ch;
             if (lane == (a.smin_wave ? (uint32_t)o : 0u) && v != ~0ull)
               atomicMin((unsigned long long*)&a.smin[slot], v);
           }
@@ -1810,7 +1836,8 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
   wave_sync();  // (the next chunk rewrites the group line)
   }
   if (a.smin) return;  // (the sample launch: no counters, no lists; no barrier follows)
-  if (valid_cnt) atomicAdd(&a.out_counters[0], (unsigned long long)valid_cnt);
+  if (valid_cnt && lane == 0) atomicAdd(&a.out_counters[0], (unsigned long long)valid_cnt);  // (uniform)
+  const uint64_t digest = *(const AS3 uint64_t*)(uintptr_t)dslot;
   if (digest) atomicAdd(&a.out_counters[1], (unsigned long long)digest);
   __syncthreads();
   Rec* dst = a.out_top + (size_t)blockIdx.x * a.n_obj * KP;

@@ -18,6 +18,8 @@
 #            PWLS (default WL), to gpurun_out/$TAG/<workload>/ (PSTEPS steps
 #            after PWARM warm-up steps, default 3 and 1; the summary leaves
 #            the warm-up launches out of its averages)
+#   summarize  scripts/summarize_profile.py of the profile step's runs (on the box, before a bench step)
+#   pin      config 5's full-size regression pin (scripts/pin_r128n6.py)
 #   trace    rocprofv3 kernel trace + stats (no counters) of bench.py for each workload in TWLS
 #   pmc      extra PMC passes: PASSES="ctr ...;ctr ..." over bench.py BENCH_ARGS
 #   shardsteps  scripts/shard_steps.py (a shard's step: wall, kernel, outside) per VARIANTS, + a trace
@@ -93,6 +95,21 @@ step_profile() {
       echo "pmc$i $wl ok"
     done
   done
+}
+
+step_summarize() {  # the profile step's summaries on the box (profiles/pmc.json, traffic.json), so that a bench step
+  # after it in the same job quotes the same build's VALU issue and traffic; re-run it here on return
+  local wl
+  for wl in ${PWLS:-${WL:-r64n7}}; do
+    timeout -k 10 120 python3 scripts/summarize_profile.py "$TAG/$wl" "${wl}_n1" > "$O/summarize_$wl.log" 2>&1 \
+      || fail "summarize $wl" $? "$O/summarize_$wl.log"
+    echo "summarize $wl ok"
+  done
+}
+
+step_pin() {  # config 5's full-size regression pin (scripts/pin_r128n6.py) to gpurun_out/$TAG/syn_r128n6_pin.json
+  timeout -k 10 600 python3 -u scripts/pin_r128n6.py "$O/syn_r128n6_pin.json" > "$O/pin.log" 2>&1 || fail pin $? "$O/pin.log"
+  echo "pin: $(tail -1 "$O/pin.log")"
 }
 
 step_trace() {  # kernel trace + stats only (no PMC), for each workload in TWLS

@@ -4,7 +4,7 @@ BOTE_KEYS_TEMPO_ALL_LEADERS) and the random R=128 n=6 windows, from the CPU
 oracle (oracle/bote_oracle.cpp compute_stats_x, checked against the oracle's
 reference-pinned single calls by tests/test_keys_oracle.py).
 
-  python tests/golden/make_keys_golden.py [--threads T] [topk|windows|all]
+  python tests/golden/make_keys_golden.py [--threads T] [topk|windows|edges|all]
 
 Writes:
   topk_x.json   every GCP R20C20 config of n = 2..13 and the synthetic
@@ -19,7 +19,13 @@ Writes:
                 with the base key set and with the extended one
                 (CONFIG5_OBJECTIVES, under "x"), the other 192 of 2.5 10^4
                 ranks with the extended key set only ("x_only": true)
-Resumable: finished windows are kept in oracle/build/keys_windows.jsonl.
+  syn_r128n6_edges.json  (round 6) a window of 10^4 ranks centred on EVERY
+                colex boundary C(m, 6), m = 6..127, where the largest member
+                changes from m - 1 to m and a new run of groups begins: each
+                swept with the base key set (DEFAULT_OBJECTIVES) and with the
+                extended one (CONFIG5_OBJECTIVES), K=32
+Resumable: finished windows are kept in oracle/build/keys_windows.jsonl
+(edges: oracle/build/keys_edges.jsonl).
 
 Data only: inputs and expected outputs.
 """
@@ -135,15 +141,59 @@ def make_windows(threads):
     json.dump(d, open(path, "w"))
 
 
+WIN_E, K_E = 10_000, 32  # the edge windows: ranks per window, top-K
+
+
+def edge_windows():
+    """[C(m, 6) - WIN_E / 2, C(m, 6) + WIN_E / 2) clipped to the rank space, m = 6..127."""
+    total = comb(128, 6)
+    return [(m, max(0, comb(m, 6) - WIN_E // 2), min(total, comb(m, 6) + WIN_E // 2)) for m in range(6, 128)]
+
+
+def make_edges(threads):
+    p = Planet.synthetic(128)
+    scratch = os.path.join(ROOT, "oracle", "build", "keys_edges.jsonl")
+    os.makedirs(os.path.dirname(scratch), exist_ok=True)
+    done = {}
+    if os.path.exists(scratch):
+        for line in open(scratch):
+            w = json.loads(line)
+            done[w["m"]] = w
+    jobs = edge_windows()
+    for m, b, e in jobs:
+        if m in done:
+            continue
+        t0 = time.time()
+        base = sweep_case(p, 6, b, e, DEFAULT_OBJECTIVES, K_E, 0, threads)
+        x = sweep_case(p, 6, b, e, objectives_x(6), K_E, 1, threads)
+        w = dict(m=m, boundary=comb(m, 6), R=128, n=6, rank_begin=b, rank_end=e, K=K_E,
+                 objectives=[list(o) for o in DEFAULT_OBJECTIVES], ranking=list(RP), ft_metric=2, **base,
+                 x=dict(keys=1, objectives=[list(o) for o in objectives_x(6)], **x))
+        w.update(cpu_seconds_wall=round(time.time() - t0, 1), threads=threads)
+        with open(scratch, "a") as fh:
+            fh.write(json.dumps(w) + "\n")
+        done[m] = w
+        print("edge", m, b, e, len(done), "/", len(jobs), round(time.time() - t0, 1), "s", flush=True)
+    d = {"what": ("oracle sweeps of 10^4-rank windows of the synthetic R=128 planet, n=6, one centred on every "
+                  "colex boundary C(m, 6), m = 6..127 (the largest member changes from m - 1 to m), with the "
+                  "base key set (DEFAULT_OBJECTIVES) and the extended key set (CONFIG5_OBJECTIVES, under \"x\"), "
+                  "K=%d, RankingParams(110,35,0,15,F1F2)" % K_E),
+         "generator": "tests/golden/make_keys_golden.py edges",
+         "windows": [done[m] for m, _, _ in jobs]}
+    json.dump(d, open(os.path.join(HERE, "syn_r128n6_edges.json"), "w"))
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("what", nargs="?", default="all", choices=["topk", "windows", "all"])
+    ap.add_argument("what", nargs="?", default="all", choices=["topk", "windows", "edges", "all"])
     ap.add_argument("--threads", type=int, default=8)
     a = ap.parse_args()
     if a.what in ("topk", "all"):
         make_topk(a.threads)
     if a.what in ("windows", "all"):
         make_windows(a.threads)
+    if a.what in ("edges", "all"):
+        make_edges(a.threads)
 
 
 if __name__ == "__main__":

@@ -82,3 +82,26 @@ def test_full_r64n7_fixture_keys_rederived():
         for key, rank in t[:20]:
             tops, _, _ = o.sweep(s, s, 7, rank, rank + 1, DEFAULT_OBJECTIVES, 1, RP, 2, 1)
             assert tops[oi] == [(key, rank)], (oi, rank)
+
+
+@pytest.mark.parametrize("m", [6, 64, 127])
+def test_r128n6_edge_windows_fixture_vs_oracle(m):
+    """tests/golden/syn_r128n6_edges.json (make_keys_golden.py edges): a
+    10^4-rank window on every colex boundary C(m, 6), m = 6..127, with both key
+    sets; three of them swept again here by the oracle."""
+    from fantoch_amd import _lib
+    from fantoch_amd.bote import CONFIG5_OBJECTIVES
+
+    fx = json.load(open(os.path.join(G, "syn_r128n6_edges.json")))
+    ws = {w["m"]: w for w in fx["windows"]}
+    assert sorted(ws) == list(range(6, 128))
+    assert all(w["rank_begin"] <= comb(mm, 6) <= w["rank_end"] for mm, w in ws.items())
+    w = ws[m]
+    p = Planet.synthetic(128)
+    o = O.OraclePlanet.of(p)
+    s = np.arange(128, dtype=np.uint32)
+    for keys, objs, c in ((0, DEFAULT_OBJECTIVES, w), (_lib.KEYS_TEMPO_ALL_LEADERS, CONFIG5_OBJECTIVES, w["x"])):
+        assert [tuple(x) for x in c["objectives"]] == list(objs)
+        tops, valid, digest = o.sweep(s, s, 6, w["rank_begin"], w["rank_end"], objs, w["K"], RP, 2, 4, keys=keys)
+        assert valid == c["valid"] and str(digest) == c["digest"]
+        assert [[[str(k), r] for k, r in t] for t in tops] == c["tops"]

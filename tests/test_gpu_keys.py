@@ -21,7 +21,8 @@ import pytest
 
 import oracle as O
 from fantoch_amd import _lib
-from fantoch_amd.bote import (CONFIG5_OBJECTIVES, DEFAULT_RANKING, DevicePlanet, MultiDeviceSearch, Sweep,
+from fantoch_amd.bote import (CONFIG5_OBJECTIVES, DEFAULT_OBJECTIVES, DEFAULT_RANKING, DevicePlanet, MultiDeviceSearch,
+                              Sweep,
                               eval_keys)
 from fantoch_amd.planet import Planet
 
@@ -222,3 +223,65 @@ def test_keys_group_client_subsets_equal_generic(R, n, nc, rb, re):
         out[k] = (r.valid, r.digest, r.tops)
     assert out["group"] == out["generic"]
     assert out["group"][0] > 0
+
+
+@pytest.mark.parametrize("keys", [0, _lib.KEYS_TEMPO_ALL_LEADERS])
+def test_group_deferred_leader_lanes_equal_generic(keys):
+    """the deferred-leader branch of the group kernel must run in a
+    test.  With the extended key set the binned client loop runs before the
+    leader choice (BIN_FIRST), so a lane whose leader decision is deferred to
+    the exact generic kernel must re-zero its member bins, or the lane's next
+    config would start from stale sums.  Planet: synthetic R=32 where regions
+    4 and 5 are twins at 200 ms from every other region and 50 ms from each
+    other: their columns have the same sum and V, their Q2 is the same, so in
+    a config holding both they tie exactly, and their near-constant columns
+    (COV close to 0) make them the best leaders: the f32 screen, then the
+    exact re-scan (cov2_sign == 0) defers the config.  The sweep must defer
+    configs (the branch ran) and still equal the exact generic kernel."""
+    base = Planet.synthetic(32)
+    lat = base.lat.astype(np.int64).copy()
+    for t in (4, 5):
+        lat[t, :] = 200
+        lat[:, t] = 200
+    lat[4, 4] = lat[5, 5] = 0
+    lat[4, 5] = lat[5, 4] = 50
+    p = Planet(base.names, lat)
+    dp = DevicePlanet(p)
+    srv = np.arange(32, dtype=np.uint32)
+    objs = CONFIG5_OBJECTIVES if keys else DEFAULT_OBJECTIVES
+    out, deferred = {}, {}
+    for k in ("group", "generic"):
+        sw = Sweep(dp, srv, srv, 6, objs, K=100, ranking=DEFAULT_RANKING, digest=True, kernel=k, keys=keys)
+        assert sw.kernel_path() == k
+        sw.launch(0, sw.total)
+        r = sw.result()
+        out[k] = (r.valid, r.digest, r.tops)
+        deferred[k] = sw.deferred()
+    assert deferred["group"] > 0, "no lane took the deferred-leader branch"
+    assert out["group"] == out["generic"]
+
+
+def test_r128n6_every_colex_boundary_vs_oracle():
+    """config 5's oracle pin at its edges.  A 10^4-rank window on
+    EVERY colex boundary C(m, 6), m = 6..127 (where the largest member changes
+    and a new run of groups starts: tests/golden/syn_r128n6_edges.json), on
+    the group kernel with the base key set and with the extended one (Tempo
+    f=1,2 + FPaxos all leaders): valid count, digest and every objective's
+    top-K equal to the oracle's."""
+    fx = _fixture("syn_r128n6_edges.json")
+    ws = fx["windows"]
+    assert sorted(w["m"] for w in ws) == list(range(6, 128))
+    p = Planet.synthetic(128)
+    dp = DevicePlanet(p)
+    srv = np.arange(128, dtype=np.uint32)
+    K = ws[0]["K"]
+    for keys, objs, sub in ((0, DEFAULT_OBJECTIVES, lambda w: w),
+                            (_lib.KEYS_TEMPO_ALL_LEADERS, CONFIG5_OBJECTIVES, lambda w: w["x"])):
+        sw = Sweep(dp, srv, srv, 6, objs, K=K, ranking=DEFAULT_RANKING, digest=True, keys=keys)
+        assert sw.kernel_path() == "group"
+        for w in ws:
+            c = sub(w)
+            sw.launch(w["rank_begin"], w["rank_end"])
+            r = sw.result()
+            assert (r.valid, str(r.digest)) == (c["valid"], c["digest"]), (keys, w["m"])
+            assert [[[str(k), rk] for k, rk in lst] for lst in r.tops] == c["tops"], (keys, w["m"])

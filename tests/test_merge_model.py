@@ -327,3 +327,33 @@ def test_wide_select_finds_a_valid_bound(seed):
     assert sum(1 for v in vals if v < x) + left == need
     y = wide_select(vals, need)[0]
     assert sum(1 for v in vals if v <= y) >= need
+
+
+@pytest.mark.parametrize("blocks", [1, 8, 32, 49])
+def test_few_lists_fall_back_to_kbound(blocks):
+    """with fewer than ceil(K / WIDE_HEAD) lists (a small grid, a
+    small shard's launch) the heads hold fewer than K records, so the heads'
+    bound never applies and the merge gathers every list's prefix at or below
+    kbound alone.  Pinned here: no head bound, the gathered count is exactly
+    the kbound prefix count, the path it takes (one pass up to WIDE_RANK_MAX
+    records, windows beyond), and the K least of the union either way."""
+    rng = np.random.default_rng(1000 + blocks)
+    K, per_block = 100, 4000
+    assert blocks * WIDE_HEAD < K
+    keys = np.sort(rng.normal(40000, 3000, size=(blocks, per_block)).astype(np.int64).clip(0), axis=1)[:, :K]
+    lists, rank = [], 0
+    for b in range(blocks):
+        lists.append([(int(k), rank + i) for i, k in enumerate(keys[b])])
+        rank += per_block
+    order = list(range(blocks))
+    random.Random(blocks).shuffle(order)
+    dumped, kb = dump(lists, K, order)
+    assert head_bound(dumped, K, kb) == (ONES, ONES)  # fewer heads than K: no bound from them
+    gathered = sum(prefix_counts(dumped, K, kb))
+    assert gathered == sum(prefix_counts(dumped, K, kb, ONES, ONES))
+    assert gathered <= blocks * K
+    path = "one pass" if gathered <= WIDE_RANK_MAX else "windows"
+    assert path == ("one pass" if blocks <= 8 else "windows"), (blocks, gathered)
+    union = sorted(r for L in lists for r in L)[:K]
+    for room in (K, 4096 - K):
+        assert wide_merge(dumped, K, kb, room) == union
