@@ -1157,6 +1157,16 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
           //      QL, high byte in byte m of QH; members 0..3 in .x, 4..6 in
           //      .y) and the colocated sums over the members
           uint2 QL[NT], QH[NT];
+          // BIN kernels with an odd number of fixed members (n = 4, 6): the
+          // two lone members, 2 and N - 1, share one table word (q_2 | q_{N-1}
+          // << 16), so the colocated sums and the bin epilogue's per-table
+          // dot products run over one word fewer (config 5, n = 6: 3 words)
+          constexpr bool PAIR2 = BIN && (F % 2 == 1);
+          constexpr int NWB = PAIR2 ? 1 + FP : 2 + FP;
+          if constexpr (PAIR2) {
+#pragma unroll
+            for (int t = 0; t < NT; ++t) wp[t][1] |= wp[t][1 + FP] << 16;
+          }
           if constexpr (PERM) {
 #pragma unroll
             for (int t = 0; t < NT; ++t) {
@@ -1169,7 +1179,7 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
               }
               uint32_t ps = 0, sq = 0;
 #pragma unroll
-              for (int i = 0; i < 2 + FP; ++i) {
+              for (int i = 0; i < NWB; ++i) {
                 ps += wp[t][i];
                 sq = __builtin_amdgcn_udot2(as_us2(wp[t][i]), as_us2(wp[t][i]), sq, false);
               }
@@ -1490,12 +1500,18 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
                 else L2 = binned_clients(BoolC<false>{}, c0, c1, c2);
                 // the bins (re-zeroed for the next config of this lane), in
                 // packed member pairs laid out as the tables' words wp[t][i]
-                // (members (0, 1), 2, (3, 4), (5, 6); a lone member's high
-                // half is don't-care: its table word's high half is 0), so
+                // (members (0, 1), 2, (3, 4), (5, 6) at n = 7; (0, 1), (2, 5),
+                // (3, 4) at n = 6, PAIR2; a lone member's high half is
+                // don't-care: its table word's high half is 0), so
                 // each table's sums are one v_dot2 per word.  The host admits
                 // the bins only where nc max < 2^16 (bote_capi.hip), so every
                 // count, every D1_m and every cnt_m q product fits a u16.
-                constexpr int NW = 2 + FP;
+                constexpr int NW = NWB;
+                // the members of word i (low, high; -1: none), as in wp[t][i]
+                auto wlo = [](int i) { return i == 0 ? 0 : (i == 1 ? 2 : 3 + 2 * (i - 2)); };
+                auto whi = [](int i) {
+                  return i == 0 ? 1 : (i == 1 ? (PAIR2 ? N - 1 : -1) : (4 + 2 * (i - 2) < N ? 4 + 2 * (i - 2) : -1));
+                };
                 uint32_t wv[N], hv[N];  // bin words; (K_m - m cnt_m) >> 4 = D1_m | cnt_m << 20
 #pragma unroll
                 for (int m = 0; m < N; ++m) {
@@ -1504,10 +1520,9 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
                   hv[m] = (m ? wv[m] - (uint32_t)m * (wv[m] >> 24) : wv[m]) >> 4;
                 }
                 uint32_t cW[NW], dW[NW];  // (cnt_m | cnt_m' << 16), (D1_m | D1_m' << 16)
-                constexpr int wlo[4] = {0, 2, 3, 5}, whi[4] = {1, -1, 4, 6};
 #pragma unroll
                 for (int i = 0; i < NW; ++i) {
-                  const int ml = wlo[i], mh = whi[i] < N ? whi[i] : -1;
+                  const int ml = wlo(i), mh = whi(i);
                   if (mh >= 0) {
                     cW[i] = __builtin_amdgcn_perm(wv[mh], wv[ml], 0x0C070C03u);
                     dW[i] = __builtin_amdgcn_perm(hv[mh], hv[ml], 0x05040100u);
@@ -1521,7 +1536,7 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
                 uint32_t L1 = 0, corr = 0;
 #pragma unroll
                 for (int i = 0; i < NW; ++i) {
-                  const int ml = wlo[i], mh = whi[i] < N ? whi[i] : -1;
+                  const int ml = wlo(i), mh = whi(i);
                   const uint32_t one = mh >= 0 ? 0x00010001u : 1u;
                   const uint32_t k32 = (uint32_t)(32 * ml) | (mh >= 0 ? (uint32_t)(32 * mh) << 16 : 0u);
                   const uint32_t kmm = (uint32_t)(ml * ml) | (mh >= 0 ? (uint32_t)(mh * mh) << 16 : 0u);

@@ -60,7 +60,7 @@ FAST_RATE, SLOW_RATE = 1.6, 0.95
 RARE_REGIONS = [
     ("if (amb) {  // exact re-scan", "leader re-scan"),
     ("PSTAT(a, 3, amb);", "leader deferred"),
-    ("if (vlead == 0.0 && Va == 0) continue;", "both COV zero (not counted: ~0)"),
+    ("if (vlead32 == 0.0f && Va == 0) continue;", "both COV zero (not counted: ~0)"),
     ("mok = (mom_mean(mf) - mom_mean(ma)) >= a.p_fmean;", "f64 mean test f=1"),
     ("if (defer) {", "validity deferred"),
 ]
@@ -206,6 +206,9 @@ def main():
                 w = 2.0 * trips * pst.get("no client lines", 0.0)
         else:
             w = 1.0
+        if os.environ.get("BOTE_MIX_BLOCKS") and w > 0:  # (diagnostics: the weighted blocks)
+            print(f"# {b} {s!r} w={w:.3f} " + " ".join(f"{k}={v}" for k, v in sorted(c.items())) +
+                  f" lines={sorted(blk_src[b])[:3]}..{sorted(blk_src[b])[-1:]}", file=sys.stderr)
         for k, v in c.items():
             dyn[s][k] += w * v
     print(f"# VALU class mix per section: `{name}`\n")

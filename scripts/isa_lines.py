@@ -11,6 +11,7 @@ default set below follows the step loop of sweep_group_kernel.  Classes as in
 scripts/isa_mix.py (measured issue rates, profiles/r02_issue_rate_ops.json).
 """
 import json
+import os
 import re
 import sys
 from collections import Counter, defaultdict
@@ -63,6 +64,17 @@ def parse(path, name, raw=False):
             # some lane takes it), even without a label
             sub += 1
             block = f"{block.split('+')[0]}+{sub}"
+    obj = os.environ.get("BOTE_ISA_OBJ")
+    if obj:
+        # DWARF inline-tree attribution (scripts/isa_attrib.py): an inlined
+        # helper's instructions go to their call line in the kernel body, not
+        # to the body line the scheduler emitted last; the object's
+        # instructions pair with this listing's by position
+        from isa_attrib import attribute
+        att = attribute(obj, name, BODY_FIRST, BODY_LAST)
+        if len(att) != len(out) or any(a[1] != o[2] for a, o in zip(att, out)):
+            sys.exit(f"{obj}: its {name} instructions differ from {path}'s (build both from one source)")
+        out = [((a[2] or o[0]),) + tuple(o[1:]) for a, o in zip(att, out)]
     return out
 
 
@@ -103,6 +115,7 @@ def default_sections():
 
 DEFAULT_SECTIONS = default_sections()
 BODY_FIRST = DEFAULT_SECTIONS[0][1]
+BODY_LAST = DEFAULT_SECTIONS[-1][2]
 
 
 def main():
