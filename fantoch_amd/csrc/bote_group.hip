@@ -293,6 +293,43 @@ __device__ __forceinline__ float cov_tf32(uint64_t tkey) {
   return (float)__longlong_as_double((long long)tkey) * (1.0f + 0x1p-10f);
 }
 
+// The 4 smallest of the union of two ascending lists A (KA real entries, the
+// rest absent) and y (KY), ascending: the elementwise minimum of A and y
+// reversed (absent entries are +inf) holds the 4 smallest as a bitonic
+// sequence (Batcher), which one bitonic merge stage of 4 compare-exchanges
+// sorts.  KA = 3, KY = 3: 2 mins + 8 ops, where the split form (merge_lists)
+// takes 15.  T: u32 or us2 (two lists at once).
+template <int KA, int KY, class T>
+__device__ __forceinline__ void merge_top4(const T* A, const T* y, T* L) {
+  static_assert(KA >= 1 && KY >= 1 && KA + KY >= 4 && KA <= 4 && KY <= 4, "4 smallest of KA + KY >= 4 entries");
+  T B[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int j = 3 - i;  // y reversed
+    if (i < KA && j < KY) B[i] = __builtin_elementwise_min(A[i < KA ? i : 0], y[j < KY ? j : 0]);
+    else if (i < KA) B[i] = A[i < KA ? i : 0];
+    else B[i] = y[j < KY ? j : 0];
+  }
+  auto ce = [&](int a, int b) {
+    const T lo = __builtin_elementwise_min(B[a], B[b]);
+    B[b] = __builtin_elementwise_max(B[a], B[b]);
+    B[a] = lo;
+  };
+  ce(0, 2);
+  ce(1, 3);
+  ce(0, 1);
+  ce(2, 3);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) L[i] = B[i];
+}
+
+// the KO smallest: merge_top4 where KO = 4 (n = 6, 7), the split form otherwise
+template <int KA, int KY, int KO, class T>
+__device__ __forceinline__ void merge_k(const T* A, const T* y, T* L) {
+  if constexpr (KO == 4 && KA + KY >= 4) merge_top4<KA, KY>(A, y, L);
+  else merge_lists<KA, KY, KO>(A, y, L);
+}
+
 // ------------------------------------------------ wave-level top-K merge --
 // Called by a whole wavefront (uniform branch).  Takes the block's LDS lock,
 // merges every lane record that beats its objective's K-th record (exact
@@ -946,6 +983,12 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
           }
           // member m: 0..2 variable, 3.. fixed (config order = ascending positions)
           uint32_t Q2[N], Q3[N];
+          // PERM: Q2 and Q3 also as the packed pair words of the rows (index
+          // as wp's: 0 members (0, 1), 1 member 2, 2 + pp fixed (3 + 2pp,
+          // 4 + 2pp); a lone member's high half 0): the leader choice reads a
+          // half with v_mad_u32_u16 op_sel, the leader's values come out by
+          // byte selection (v_perm), so neither needs the unpacked values
+          uint32_t Q2w[4] = {0u, 0u, 0u, 0u}, Q3w[4] = {0u, 0u, 0u, 0u};
           uint32_t cS1p = 0, cS1e = 0;  // colocated sums: packed (t0 | t1 << 16), third table
           uint32_t cS2[NT], cS1t[NT];  // (PERM: per table)
 #pragma unroll
@@ -967,6 +1010,8 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
               const uint32_t hm = has_hi ? ~0u : 0xFFFFu;
 #pragma unroll
               for (int t = 0; t < NT; ++t) wp[t][pi] = L[QT::q(t) - 2] & hm;
+              Q2w[pi] = L[0] & hm;
+              Q3w[pi] = L[1] & hm;
               (void)w0;
               (void)w1;
               return;
@@ -1026,7 +1071,7 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
 #pragma unroll
                 for (int k = 0; k < KQ; ++k) L[k] = pk_min(A[k], y[k & 1]);
               } else {
-                merge_lists<F < 4 ? F : 4, 2, KQ>(A, y, L);
+                merge_k<F < 4 ? F : 4, 2, KQ>(A, y, L);
               }
               uint32_t W[KQ];
 #pragma unroll
@@ -1042,7 +1087,7 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
               const uint32_t d20 = l16(cv[0] + 2 * rv[2]) >> LAT_SHIFT, d21 = l16(cv[1] + 2 * rv[2]) >> LAT_SHIFT;
               y[0] = min(d20, d21);
               y[1] = max(d20, d21);
-              merge_lists<F < 4 ? F : 4, 2, KQ>(A, y, L);
+              merge_k<F < 4 ? F : 4, 2, KQ>(A, y, L);
               emit_pk(2, false, L);
             }
 #pragma unroll
@@ -1071,7 +1116,9 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
 #pragma unroll
                 for (int k = 0; k < KQ; ++k) L[k] = pk_min(A[k], y[k < 3 ? k : 2]);
               } else {
-                merge_lists<KQ, 3, KQ>(A, y, L);
+                // (the group's fixed-row lists hold F - 1 real distances, the
+                // self entry and padding sort last as +inf)
+                merge_k<(F - 1 < KQ ? F - 1 : KQ), 3, KQ>(A, y, L);
               }
               uint32_t W[KQ];
 #pragma unroll
@@ -1206,6 +1253,25 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
           // below m (exact zeros, V = 0, t = inf, tie exactly and keep the
           // first, as the reference's first-minimum does).
           uint32_t bi = 0;
+          // PERM (n <= 7): the leader's byte code, member l -> l + (l >= 3),
+          // so that codes 0..2 name the bytes of the step's packed variable
+          // positions (cur) and 4..7 those of the packed fixed ones, and a
+          // code's low 2 bits index its member within the Q2w / Q3w byte pool
+          uint32_t lcode = 0;
+          auto code_of = [](int l) { return (uint32_t)(l + (l >= 3 ? 1 : 0)); };
+          // S = s1 + nc Q2 for member l from its packed word (op_sel: the half)
+          auto s_of = [&](int l) {
+            if constexpr (PERM) {
+              const int pi = l < 2 ? 0 : (l == 2 ? 1 : 2 + (l - 3) / 2);
+              const bool hi = l < 2 ? l == 1 : (l > 2 && (l - 3) % 2 == 1);
+              uint32_t r;
+              if (hi) asm("v_mad_u32_u16 %0, %1, %2, %3 op_sel:[1,0,0,0]" : "=v"(r) : "v"(Q2w[pi]), "s"(nc), "v"(s1_of(l)));
+              else asm("v_mad_u32_u16 %0, %1, %2, %3" : "=v"(r) : "v"(Q2w[pi]), "s"(nc), "v"(s1_of(l)));
+              return r;
+            } else {
+              return s1_of(l) + __umul24(nc, Q2[l]);
+            }
+          };
           bool amb = false;
           if (!ABLATE(a, 128)) {
             // t >= 0 and never NaN here (S >= nc * Q2 > 0: server-server
@@ -1218,8 +1284,8 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
             uint32_t u[N];
 #pragma unroll
             for (int l = 0; l < N; ++l) {
-              const float t = (float)(s1_of(l) + __umul24(nc, Q2[l])) * wf_of(l);
-              u[l] = (__float_as_uint(t) & ~IM) | (IM - (uint32_t)l);
+              const float t = (float)s_of(l) * wf_of(l);
+              u[l] = (__float_as_uint(t) & ~IM) | (IM - (PERM ? code_of(l) : (uint32_t)l));
             }
             // the largest and second largest (with multiplicity) t: a
             // running max and median-of-three, 2 ops per member
@@ -1230,6 +1296,10 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
               mu = max(mu, u[l]);
             }
             bi = (mu & IM) ^ IM;  // the first member at the maximum
+            if constexpr (PERM) {
+              lcode = bi;
+              bi = lcode - (lcode >> 2);  // (codes 4..7: members 3..6)
+            }
             const float m = __uint_as_float(mu & ~IM), m2 = __uint_as_float(m2u & ~IM);
             amb = m < __builtin_inff() && m2 >= m * (1.0f - 0x1p-18f);
           }
@@ -1237,6 +1307,7 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
           if (amb) {  // exact re-scan in the generic path's arithmetic
             amb = false;
             bi = 0;
+            lcode = 0;
             uint32_t bpos = pv[0];
             uint32_t bS = s1_of(0) + nc * Q2[0];
             float bV = vf_of(0);
@@ -1250,6 +1321,7 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
               if (c == 0) amb = true;
               if (c < 0) {
                 bi = l;
+                lcode = code_of(l);
                 bS = S;
                 bV = V;
                 bpos = pl;
@@ -1268,14 +1340,31 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
           }
           if (have) {
             uint32_t lpos = pv[0], lq2 = Q2[0], lq3 = Q3[0], lreg = rv[0];
+            if constexpr (PERM && SI) {
+              // the leader's values by byte selection on its code: Q2 / Q3
+              // from the pool of members 0..2 (Q2w[0..1]) or 3..6 (Q2w[2..3]),
+              // 2 bytes at 2 (code & 3); its position from the step's packed
+              // variable positions (cur: p0 | p1 << 8 | p2 << 16) or the
+              // group's fixed ones (hqw); 11 ops where the compare/select
+              // chain over the members took 28
+              uint32_t hqw = 0;
 #pragma unroll
-            for (int l = 1; l < N; ++l)
-              if (bi == (uint32_t)l) {
-                lpos = pos_of(l);
-                lq2 = Q2[l];
-                lq3 = Q3[l];
-                if constexpr (!SI) lreg = reg_of(l);
-              }
+              for (int k = 0; k < F; ++k) hqw |= hq[k] << (8 * k);
+              const uint32_t sel = 0x0C0C0100u + (lcode & 3u) * 0x0202u;
+              const bool pb = lcode >= 4u;
+              lq2 = pb ? __builtin_amdgcn_perm(Q2w[3], Q2w[2], sel) : __builtin_amdgcn_perm(Q2w[1], Q2w[0], sel);
+              lq3 = pb ? __builtin_amdgcn_perm(Q3w[3], Q3w[2], sel) : __builtin_amdgcn_perm(Q3w[1], Q3w[0], sel);
+              lpos = __builtin_amdgcn_perm(hqw, cur, 0x0C0C0C00u | lcode);
+            } else {
+#pragma unroll
+              for (int l = 1; l < N; ++l)
+                if (bi == (uint32_t)l) {
+                  lpos = pos_of(l);
+                  lq2 = Q2[l];
+                  lq3 = Q3[l];
+                  if constexpr (!SI) lreg = reg_of(l);
+                }
+            }
             if constexpr (SI) lreg = lpos;  // (servers in region order: position = region)
             Mom mom[NSLOT];
             // XK: the extended slots and every leader's FPaxos moments are

@@ -72,6 +72,7 @@ def parse(path, name, raw=False):
         # instructions pair with this listing's by position
         from isa_attrib import attribute
         att = attribute(obj, name, BODY_FIRST, BODY_LAST)
+        att = att[:len(out)]  # (the object may decode alignment padding after the kernel's last instruction)
         if len(att) != len(out) or any(a[1] != o[2] for a, o in zip(att, out)):
             sys.exit(f"{obj}: its {name} instructions differ from {path}'s (build both from one source)")
         out = [((a[2] or o[0]),) + tuple(o[1:]) for a, o in zip(att, out)]
