@@ -124,18 +124,26 @@ def attribute(obj_path, name, body_first, body_last, main="bote_group.hip"):
     def in_body(f, ln):
         return f is not None and f.endswith(main) and body_first <= ln <= body_last
 
+    # one-line lambdas of the body (`auto s1_of = [&](int l) { ... };`): their
+    # instructions are charged to the call, like a helper's (a lambda that
+    # only a rare branch calls is then rare, not charged to its definition)
+    src = open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "fantoch_amd", "csrc",
+                            main)).read().split("\n")
+    one_line = {i + 1 for i, l in enumerate(src) if re.search(r"=\s*\[[&=]?\]\s*\(.*\{.*\};\s*(//.*)?$", l)}
+
     out = []
     for a, op in ins:
         i = bisect.bisect_right(addrs, a) - 1
         f, ln = (files.get(rows[i][1]), rows[i][2]) if i >= 0 else (None, 0)
-        if in_body(f, ln):
+        if in_body(f, ln) and ln not in one_line:
             out.append((a, op, ln))
             continue
-        best, bd = 0, -1  # the innermost containing call whose site is in the body
+        best, bd = 0, -1  # the innermost containing call whose site is in the body (and not a one-line lambda)
         for t in tree:
-            if t["depth"] > bd and in_body(t["file"], t["line"]) and any(x <= a < y for x, y in t["ranges"]):
+            if t["depth"] > bd and in_body(t["file"], t["line"]) and t["line"] not in one_line and \
+                    any(x <= a < y for x, y in t["ranges"]):
                 best, bd = t["line"], t["depth"]
-        out.append((a, op, best))
+        out.append((a, op, best or (ln if in_body(f, ln) else 0)))
     return out
 
 
