@@ -552,11 +552,13 @@ def main():
                          "work_per_config": issued,
                          "work_def": "issued VALU lane-ops per config: SQ_INSTS_VALU per 64-config wave step x 64 lanes / 64 "
                                      "(profiles/pmc.json, same build only; DESIGN.md §5)",
-                         "w_prime": {"per_config": Wg, "frac": shard * Wg / (kavg_ms * 1e-3) / 1e12 / VALU_PEAK_TOPS,
-                                     "def": "W' (DESIGN.md §5, bench.work_per_config_%s): algorithmic ops, several "
-                                            "per packed instruction; not a utilisation" % (
+                         # (W' and SURVEY's W count algorithmic ops, several per packed
+                         # instruction: reported as counts, never priced against the VALU peak)
+                         "w_prime": {"per_config": Wg, "per_issued_lane_op": Wg / issued if issued else None,
+                                     "def": "W' (DESIGN.md §5, bench.work_per_config_%s): algorithmic ops per config, "
+                                            "several per packed instruction; a count, not a roofline" % (
                                                 "keys" if wl["keys"] else "group")},
-                         "survey_w": W, "survey_w_frac": shard * W / (kavg_ms * 1e-3) / 1e12 / VALU_PEAK_TOPS,
+                         "survey_w": W,
                          "valu_issue": valu, "kernel_ms_avg": kavg_ms,
                          # VALU issue (SQ_INSTS_VALU x 2 cycles over SIMD-cycles at the PMC run's clock):
                          # frac above at the nominal 2.4 GHz

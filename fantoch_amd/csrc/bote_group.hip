@@ -417,6 +417,22 @@ __device__ __forceinline__ int cov2_sign(float Vx, uint32_t Sx, float Vy, uint32
   return D < -T ? -1 : (D > T ? 1 : 0);
 }
 
+// The validity form (cov_f >= cov_a): the same band, decided with one
+// product per side, x (1 - 2^-18) >= y and x < y (1 - 2^-18), so that both V
+// zero (COV 0 >= COV 0) is decided 1 by the screen itself
+template <class FX, class FY>
+__device__ __forceinline__ int cov2_sign_ge(float Vx, uint32_t Sx, float Vy, uint32_t Sy, const FX& dVx, const FY& dVy) {
+  const float fx = (float)Sx, fy = (float)Sy;
+  const float x = Vx * (fy * fy), y = Vy * (fx * fx);
+  constexpr float c = 1.0f - 0x1p-18f;
+  if (x * c >= y) return 1;
+  if (x < y * c) return -1;
+  const double sx = (double)Sx, sy = (double)Sy;
+  const double X = dVx() * (sy * sy), Y = dVy() * (sx * sx);
+  const double D = X - Y, T = 0x1p-32 * fmax(X, Y);
+  return D < -T ? -1 : (D > T ? 1 : 0);
+}
+
 // u64 -> f32 in three instructions (two conversions and an fma): within
 // 2^-23 relative, inside the screens' error budget
 __device__ __forceinline__ float u64_to_f32(uint64_t x) {
@@ -505,6 +521,7 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
   tk.cand = (Rec*)(smem + off[10]);
   tk.tmp = (Rec*)(smem + off[11]);
   tk.thr = (Rec*)(smem + off[12]);
+  const uint32_t thra = LB + (uint32_t)off[12];  // (the thresholds' LDS address)
   tk.cnt = nullptr;
   int* lock = (int*)(smem + off[13]);
   const uint32_t tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, BD = blockDim.x, WPB = BD >> 6;
@@ -581,9 +598,15 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
   // step, scalar adds) and each lane's running digest in LDS (off[15]):
   // neither holds vector registers across the step loop
   uint64_t valid_cnt = 0;
-  const uint32_t dslot = LB + (uint32_t)off[15] + tid * 8;
-  auto digest_add = [&](uint64_t d) {
-    __hip_atomic_fetch_add((AS3 uint64_t*)(uintptr_t)dslot, d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+  // (the slot address is rebuilt at each add from the bins' lane address,
+  // binb = LB + off[14] + 256 N wid + 4 lane, live through the step anyway:
+  // the slot's own address, live across the step loop, was spilled and
+  // reloaded from scratch every step)
+  const uint32_t dofs = uni(LB + (uint32_t)off[15] + wid * 512u - 2u * (LB + (uint32_t)off[14] + wid * (N * 256u)));
+  auto digest_add = [&](uint32_t binb_, uint64_t d) {
+    uint32_t ad;
+    asm("v_lshl_add_u32 %0, %1, 1, %2" : "=v"(ad) : "v"(binb_), "s"(dofs));
+    __hip_atomic_fetch_add((AS3 uint64_t*)(uintptr_t)ad, d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
   };
 
   // Work: either this wave's equal share of [rb, re), or (nwchunks > 0)
@@ -720,6 +743,22 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
           sort_network<4>(rf);
           s128(rxt + 16 * x, make_uint4(rf[0] | (rf[1] << 16), rf[2] | (rf[3] << 16), cf[0] | (cf[1] << 16),
                                         cf[2] | (cf[3] << 16)));
+        }
+        // a fixed member's row at its own position (no variable member sits
+        // there): the column part only, its distances to the fixed members,
+        // itself included; the colocated leader-column sums read the leader's
+        // row whichever member leads
+        if (lane < (uint32_t)F) {
+          uint32_t rj = 0, pj = 0;
+#pragma unroll
+          for (int k = 0; k < F; ++k) {
+            rj = lane == (uint32_t)k ? freg[k] : rj;
+            pj = lane == (uint32_t)k ? hq[k] : pj;
+          }
+          uint32_t cf[4];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) cf[k] = k < F ? l16(rqt + rj * rstride + 2 * freg[k < F ? k : 0]) >> LAT_SHIFT : 0xFFFFu;
+          s64(rxt + 16 * pj + 8, cf[0] | (cf[1] << 16), cf[2] | (cf[3] << 16));
         }
       }
       wave_sync();
@@ -934,17 +973,24 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
             const uint32_t nql = ABLATE(a, 1) ? 0u : nq;
             const uint32_t kfl = a.k_flush, fU = kfl / UB ? kfl / UB : 1u;
             uint32_t g = 0, k = 0;
+            auto ub_body = [&](uint32_t g0) {
+              uint32_t Lk[UB], Hk[UB];
+#pragma unroll
+              for (uint32_t u = 0; u < UB; u += 2) nearest2(g0 * 8 + 8 * u, Lk[u], Hk[u], Lk[u + 1], Hk[u + 1]);
+#pragma unroll
+              for (uint32_t u = 0; u < UB; ++u) quad_bin(Lk[u], Hk[u], 4u);
+            };
             if (kfl >= nql + UB) {
               // one 32-bit sum holds every client's squared key: no flush test
               // in the loop (a uniform branch; at R=64 the test cost two VCC
-              // v_cndmask and a 64-bit add per iteration)
-              for (; g + UB <= nql; g += UB) {
-                uint32_t Lk[UB], Hk[UB];
-#pragma unroll
-                for (uint32_t u = 0; u < UB; u += 2) nearest2(g * 8 + 8 * u, Lk[u], Hk[u], Lk[u + 1], Hk[u + 1]);
-#pragma unroll
-                for (uint32_t u = 0; u < UB; ++u) quad_bin(Lk[u], Hk[u], 4u);
+              // v_cndmask and a 64-bit add per iteration).  Two bodies per
+              // trip: the second's reads take immediate offsets, so the lane
+              // addresses advance once per 2 UB quads
+              for (; g + 2 * UB <= nql; g += 2 * UB) {
+                ub_body(g);
+                ub_body(g + UB);
               }
+              for (; g + UB <= nql; g += UB) ub_body(g);
             } else if (kfl >= UB) {
               for (; g + UB <= nql; g += UB) {
                 uint32_t Lk[UB], Hk[UB];
@@ -1695,9 +1741,26 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
               const uint32_t lcol = __umul24(lreg, rstride) + rqt;
               // sum_k (v_k + q) and sum_k (v_k + q)^2 from sum v and sum v^2
               uint32_t sv = 0, sv2 = 0;
+              int k0 = 0;
+              if (use_rx) {
+                // the fixed members' part from the column words of the
+                // leader's position-table row (packed u16 pairs: v_dot2; the
+                // pad halves past F are INF and masked off), then the three
+                // variable members' distances
+                const uint2 cw = l64(rxt + 16 * lpos + 8);
+                const uint32_t w0 = F >= 2 ? cw.x : (cw.x & 0xFFFFu), w1 = F >= 4 ? cw.y : (cw.y & 0xFFFFu);
+                sv = __builtin_amdgcn_udot2(as_us2(w0), as_us2(0x00010001u), 0u, false);
+                sv2 = __builtin_amdgcn_udot2(as_us2(w0), as_us2(w0), 0u, false);
+                if constexpr (F >= 3) {
+                  sv = __builtin_amdgcn_udot2(as_us2(w1), as_us2(0x00010001u), sv, false);
+                  sv2 = __builtin_amdgcn_udot2(as_us2(w1), as_us2(w1), sv2, false);
+                }
+                k0 = 3;
+              }
 #pragma unroll
               for (int k = 0; k < N; ++k) {
                 if (ABLATE(a, 512)) break;
+                if (k >= 3 && k0 == 3) break;
                 const uint32_t v = l16(lcol + 2 * reg_of(k)) >> LAT_SHIFT;
                 sv += v;
                 sv2 += v * v;
@@ -1787,8 +1850,7 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
                     uint64_t Va = Va1;
                     float vaf = va1;
                     if (f != 1) vmom(ma, Va, vaf);
-                    if (vlead32 == 0.0f && Va == 0) continue;  // both COV 0
-                    const int c = cov2_sign(vlead32, (uint32_t)mf.s1, vaf, (uint32_t)ma.s1, [&] { return vcol[lpos]; },
+                    const int c = cov2_sign_ge(vlead32, (uint32_t)mf.s1, vaf, (uint32_t)ma.s1, [&] { return vcol[lpos]; },
                                             [&] { return (double)Va; });
                     lt = lt || c < 0;
                     amb_c = amb_c || c == 0;
@@ -1806,7 +1868,7 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
                   uint32_t h = hx;  // (0 without XK)
 #pragma unroll
                   for (int sl = 0; sl < NSLOT; ++sl) h = digest_fold(h, sl, mom[sl].s1, mom[sl].s2);
-                  digest_add(digest_final(rank, bi, h));
+                  digest_add(binb, digest_final(rank, bi, h));
                 }
                 // ---- default objectives: 0 SCORE, 1 MEAN af1, 2 MEAN ff1, 3 COV af1, 4 MEAN e
                 if (ABLATE(a, 2048)) valid = false;
@@ -1869,7 +1931,7 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
               if (!finish_config<N>(a, mom, vcol[lpos], bi, rank, tk.thr, pnc1, pnc2, vc, dg, key, ok) && !a.smin)
                 defer_rank(a, rank);
               vflag = vc != 0;
-              if (dg) digest_add(dg);
+              if (dg) digest_add(binb, dg);
             }
           }
         }
@@ -1902,10 +1964,20 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
           }
         } else if (!ABLATE(a, 4)) {
           const int nobj = XK ? 8 : (DEF ? 5 : a.n_obj);
+          // (the thresholds read first, from one LDS address with immediate
+          // offsets: read under the short-circuit test, each cost a spilled
+          // SGPR reload and an address move)
+          uint64_t th[MAXOBJ];
+#pragma unroll
+          for (int o = 0; o < MAXOBJ; ++o)
+            if (o < nobj) {
+              const uint2 t = l64(thra + 16u * o);
+              th[o] = ((uint64_t)t.y << 32) | t.x;
+            }
           bool pass = false;
 #pragma unroll
           for (int o = 0; o < MAXOBJ; ++o)
-            if (o < nobj) pass = pass || (ok[o] && key[o] <= tk.thr[o].key);
+            if (o < nobj) pass = pass || (ok[o] && key[o] <= th[o]);
           PSTAT(a, 11, pass);  // block top-K merge
           if (__ballot(pass)) wave_topk(tk, lock, a.nc, nobj, a.K, key, ok, rank);
         }
@@ -1941,7 +2013,7 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
   }
   if (a.smin) return;  // (the sample launch: no counters, no lists; no barrier follows)
   if (valid_cnt && lane == 0) atomicAdd(&a.out_counters[0], (unsigned long long)valid_cnt);  // (uniform)
-  const uint64_t digest = *(const AS3 uint64_t*)(uintptr_t)dslot;
+  const uint64_t digest = *(const AS3 uint64_t*)(uintptr_t)(LB + (uint32_t)off[15] + tid * 8);
   if (digest) atomicAdd(&a.out_counters[1], (unsigned long long)digest);
   __syncthreads();
   Rec* dst = a.out_top + (size_t)blockIdx.x * a.n_obj * KP;

@@ -6,8 +6,8 @@ per 64-config step, reconciled against the measured SQ_INSTS_VALU.
   BOTE_PSTATS=<pathstats json> python scripts/class_mix_table.py kg.s ILi7ELb1ELb1ELb1ELb0ELb1E profiles/pmc.json \
       r64n7_n1 > profiles/<tag>_class_mix.md
   (optional 5th-7th arguments: R n trips -- the workload, and the client
-  loop's unrolled-body trips per step: nq / U; default 64 7 4; the config-5
-  kernel, -DBOTE_ISA_N6: ... r128n6_n1 128 6 8)
+  loop's unrolled-body trips per step: nq / (2 BIN_UB), two bodies per trip;
+  default 64 7 2; the config-5 kernel, -DBOTE_ISA_N6: ... r128n6_n1 128 6 4)
 
 Static: instructions per section (scripts/isa_lines.py markers).  Modelled
 dynamic count per step: every basic block of a per-step section runs once per
@@ -60,7 +60,6 @@ FAST_RATE, SLOW_RATE = 1.6, 0.95
 RARE_REGIONS = [
     ("if (amb) {  // exact re-scan", "leader re-scan"),
     ("PSTAT(a, 3, amb);", "leader deferred"),
-    ("if (vlead32 == 0.0f && Va == 0) continue;", "both COV zero (not counted: ~0)"),
     ("mok = (mom_mean(mf) - mom_mean(ma)) >= a.p_fmean;", "f64 mean test f=1"),
     ("if (defer) {", "validity deferred"),
 ]
@@ -95,7 +94,7 @@ def main():
     # regions and the no-lines client loop are weighted by them; without it,
     # every rare region weighs 0 as before
     pst = json.load(open(os.environ["BOTE_PSTATS"]))["per_step"] if os.environ.get("BOTE_PSTATS") else {}
-    R, n, trips = (int(x) for x in sys.argv[5:8]) if len(sys.argv) > 7 else (64, 7, 4)
+    R, n, trips = (int(x) for x in sys.argv[5:8]) if len(sys.argv) > 7 else (64, 7, 2)
     groups, steps = comb(R - 3, n - 3), comb(R, n) / 64.0  # groups: the fixed parts above position 3
     per_step_groups = groups / steps
     rows = parse(path, name, raw=True)
@@ -114,7 +113,10 @@ def main():
     merge_blk = set()
     own_line = defaultdict(bool)  # a block with instructions from bote_group.hip lines
     order = []
+    blk_opl = defaultdict(list)
+    hotl = Counter()
     for ln, b, op, raw_ln in rows:
+        blk_opl[b].append((ln, op))
         if b not in blk_ops:
             order.append(b)
         blk_ops[b].append(op)
@@ -211,6 +213,17 @@ def main():
                   f" lines={sorted(blk_src[b])[:3]}..{sorted(blk_src[b])[-1:]}", file=sys.stderr)
         for k, v in c.items():
             dyn[s][k] += w * v
+        if w > 0 and os.environ.get("BOTE_MIX_LINE"):  # (diagnostics: one line's weighted instructions)
+            sel = [o for ln_, o in blk_opl[b] if str(ln_) == os.environ["BOTE_MIX_LINE"]]
+            if sel:
+                print(f"# {b} w={w:.3f} " + " ".join(sel), file=sys.stderr)
+        if w > 0:
+            for (ln_, o) in blk_opl[b]:
+                if classify(o) in ("valu_fast", "valu_slow", "spill_lane"):
+                    hotl[ln_] += w
+    if os.environ.get("BOTE_MIX_LINES"):  # (diagnostics: the heaviest source lines, VALU per step)
+        for ln_, v in hotl.most_common(int(os.environ["BOTE_MIX_LINES"])):
+            print(f"# {v:6.1f}  {ln_:5d}  {src[ln_ - 1].strip()[:110] if ln_ else '?'}", file=sys.stderr)
     print(f"# VALU class mix per section: `{name}`\n")
     print("Static instructions from the device assembly (`-g` line info, scripts/isa_lines.py sections);")
     print("modelled per 64-config step as described in scripts/class_mix_table.py.  Fast class")
@@ -235,7 +248,8 @@ def main():
     print(f"| **total** | | | {tot['valu_fast']:.0f} | {tot['valu_slow']:.0f} | {tot['spill_lane']:.0f} | "
           f"{allc:.0f} | |\n")
     print(f"Modelled VALU instructions per step (fast + slow + spill-lane moves): **{model:.0f}**; "
-          f"slow share {(tot['valu_slow'] + tot['spill_lane']) / model:.1%}.")
+          f"slow share {(tot['valu_slow'] + tot['spill_lane']) / model:.1%}; scratch accesses per step "
+          f"{tot['scratch']:.2f}, LDS {tot['lds']:.0f}.")
     if pmc:
         meas = pmc["valu_insts_per_config"]
         # wavefront steps actually run per 64 configs: a group of C(p3, 3) configs takes ceil(/64) steps

@@ -83,7 +83,7 @@ def parse(path, name, raw=False):
 MARKERS = [
     ("setup+chunks", "sweep_group_kernel(FastArgs a) {"),
     ("group precompute", "// ---------------- per-group, wave-uniform precompute"),
-    ("step head (lowtab, keys init)", "// ---------------- the group's configs, 64 per step"),
+    ("step head (lowtab, keys init)", "while (left) {"),
     ("client lines build", "// ---- PERM: client lines."),
     ("step members (unpack)", "uint32_t pv[3], rv[3];"),
     # the member-binned client loop's one body (a lambda: its instructions
@@ -100,7 +100,7 @@ MARKERS = [
     ("digest", "if ((SI || a.want_digest) && !ABLATE(a, 16))"),
     ("objective keys + score", "// ---- default objectives: 0 SCORE"),
     ("top-K screen + merge", "// ---- top-K: lock-free screen"),
-    ("next group", "// ---------------- next group"),
+    ("next group", "// (a sample chunk stops at its first group"),
     (None, "// ------------------------------------------------------------- launcher"),
 ]
 
