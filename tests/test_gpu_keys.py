@@ -22,8 +22,7 @@ import pytest
 import oracle as O
 from fantoch_amd import _lib
 from fantoch_amd.bote import (CONFIG5_OBJECTIVES, DEFAULT_OBJECTIVES, DEFAULT_RANKING, DevicePlanet, MultiDeviceSearch,
-                              Sweep,
-                              eval_keys)
+                              Sweep, eval_keys)
 from fantoch_amd.planet import Planet
 
 pytestmark = pytest.mark.gpu
@@ -285,3 +284,24 @@ def test_r128n6_every_colex_boundary_vs_oracle():
             r = sw.result()
             assert (r.valid, str(r.digest)) == (c["valid"], c["digest"]), (keys, w["m"])
             assert [[[str(k), rk] for k, rk in lst] for lst in r.tops] == c["tops"], (keys, w["m"])
+
+
+def test_r128n6_windows_around_the_pin_vs_oracle():
+    """The oracle's windows of 2 x 2,048 ranks around every record of config
+    5's full-size regression pin (tests/golden/syn_r128n6_around_pin.json, 538
+    merged windows, 2.3e6 configs), swept by the group kernel with the
+    extended key set: valid count, digest and every objective's top-100 equal
+    the oracle's."""
+    fx = _fixture("syn_r128n6_around_pin.json")
+    p = Planet.synthetic(128)
+    dp = DevicePlanet(p)
+    srv = np.arange(128, dtype=np.uint32)
+    sw = Sweep(dp, srv, srv, 6, CONFIG5_OBJECTIVES, K=fx["K"], ranking=DEFAULT_RANKING, digest=True,
+               keys=_lib.KEYS_TEMPO_ALL_LEADERS)
+    assert sw.kernel_path() == "group"
+    assert [tuple(o) for o in fx["objectives"]] == list(CONFIG5_OBJECTIVES)
+    for w in fx["windows"]:
+        sw.launch(w["rank_begin"], w["rank_end"])
+        r = sw.result()
+        assert (r.valid, str(r.digest)) == (w["valid"], w["digest"]), w["rank_begin"]
+        assert [[[str(k), rk] for k, rk in lst] for lst in r.tops] == w["tops"], w["rank_begin"]
