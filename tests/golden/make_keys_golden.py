@@ -4,7 +4,7 @@ BOTE_KEYS_TEMPO_ALL_LEADERS) and the random R=128 n=6 windows, from the CPU
 oracle (oracle/bote_oracle.cpp compute_stats_x, checked against the oracle's
 reference-pinned single calls by tests/test_keys_oracle.py).
 
-  python tests/golden/make_keys_golden.py [--threads T] [topk|windows|edges|all]
+  python tests/golden/make_keys_golden.py [--threads T] [topk|windows|edges|around|all]
 
 Writes:
   topk_x.json   every GCP R20C20 config of n = 2..13 and the synthetic
@@ -24,8 +24,14 @@ Writes:
                 changes from m - 1 to m and a new run of groups begins: each
                 swept with the base key set (DEFAULT_OBJECTIVES) and with the
                 extended one (CONFIG5_OBJECTIVES), K=32
+  syn_r128n6_around_pin.json  (round 6) a window of 2 x 2,048 ranks around
+                every record of the full-size regression pin
+                (syn_r128n6_pin.json: 8 objectives x 100), overlapping ones
+                merged, swept with the extended key set (CONFIG5_OBJECTIVES,
+                K=100): the oracle's view of the pin's records and of their
+                colex neighbours
 Resumable: finished windows are kept in oracle/build/keys_windows.jsonl
-(edges: oracle/build/keys_edges.jsonl).
+(edges: oracle/build/keys_edges.jsonl; around: keys_around.jsonl).
 
 Data only: inputs and expected outputs.
 """
@@ -183,9 +189,77 @@ def make_edges(threads):
     json.dump(d, open(os.path.join(HERE, "syn_r128n6_edges.json"), "w"))
 
 
+A_P = 2_048  # the windows around the pin's records: ranks on each side
+KEEP_A = 8  # records kept per window list at least
+
+
+def around_windows():
+    """[rank - A_P, rank + A_P) around every record of syn_r128n6_pin.json
+    (8 objectives x 100), clipped to the rank space, overlapping ones merged."""
+    pin = json.load(open(os.path.join(HERE, "syn_r128n6_pin.json")))
+    total = comb(128, 6)
+    iv = sorted((max(0, r - A_P), min(total, r + A_P)) for t in pin["tops"] for _, r in t)
+    out = []
+    for b, e in iv:
+        if out and b <= out[-1][1]:
+            out[-1][1] = max(out[-1][1], e)
+        else:
+            out.append([b, e])
+    return [tuple(x) for x in out]
+
+
+def make_around(threads):
+    p = Planet.synthetic(128)
+    scratch = os.path.join(ROOT, "oracle", "build", "keys_around.jsonl")
+    os.makedirs(os.path.dirname(scratch), exist_ok=True)
+    done = {}
+    if os.path.exists(scratch):
+        for line in open(scratch):
+            w = json.loads(line)
+            done[(w["rank_begin"], w["rank_end"])] = w
+    jobs = around_windows()
+    t_all = time.time()
+    for b, e in jobs:
+        if (b, e) in done:
+            continue
+        x = sweep_case(p, 6, b, e, objectives_x(6), 100, 1, threads)
+        w = dict(rank_begin=b, rank_end=e, **x)
+        with open(scratch, "a") as fh:
+            fh.write(json.dumps(w) + "\n")
+        done[(b, e)] = w
+        if len(done) % 50 == 0:
+            print("around", len(done), "/", len(jobs), round(time.time() - t_all, 1), "s", flush=True)
+    # each window's lists are kept up to one record past the pin's K-th
+    # (key, rank) of the objective, and at least KEEP_A records: every window
+    # config at or below that record is kept, and the rest of a K=100 list is
+    # prefix-checked on the GPU
+    pin = json.load(open(os.path.join(HERE, "syn_r128n6_pin.json")))
+    kth = [(int(t[-1][0]), t[-1][1]) for t in pin["tops"]]
+    wins = []
+    for b, e in jobs:
+        w = dict(done[(b, e)])
+        tops, full = [], []
+        for o, t in enumerate(w["tops"]):
+            below = sum(1 for k, r in t if (int(k), r) <= kth[o])
+            full.append(below == len(t) == 100)  # (a K=100 list entirely at or below the K-th: more may exist)
+            tops.append(t[:max(KEEP_A, below + 1)])
+        w["tops"], w["full_below_kth"] = tops, full
+        wins.append(w)
+    d = {"what": ("oracle sweeps (extended key set, CONFIG5_OBJECTIVES, K=100, RankingParams(110,35,0,15,F1F2)) of "
+                  "the synthetic R=128 planet, n=6, over a window of %d ranks on each side of every record of "
+                  "syn_r128n6_pin.json (8 objectives x 100 records; overlapping windows merged): the pin's "
+                  "records and their colex neighbours, where their closest competitors are.  Each objective's "
+                  "K=100 list is kept up to one record past the pin's 100th (key, rank) and at least %d records "
+                  "(a prefix of the oracle's list)" % (A_P, KEEP_A)),
+         "generator": "tests/golden/make_keys_golden.py around",
+         "R": 128, "n": 6, "keys": 1, "K": 100, "objectives": [list(o) for o in objectives_x(6)],
+         "windows": wins}
+    json.dump(d, open(os.path.join(HERE, "syn_r128n6_around_pin.json"), "w"))
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("what", nargs="?", default="all", choices=["topk", "windows", "edges", "all"])
+    ap.add_argument("what", nargs="?", default="all", choices=["topk", "windows", "edges", "around", "all"])
     ap.add_argument("--threads", type=int, default=8)
     a = ap.parse_args()
     if a.what in ("topk", "all"):
@@ -194,6 +268,8 @@ def main():
         make_windows(a.threads)
     if a.what in ("edges", "all"):
         make_edges(a.threads)
+    if a.what in ("around", "all"):
+        make_around(a.threads)
 
 
 if __name__ == "__main__":

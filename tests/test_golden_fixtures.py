@@ -105,3 +105,62 @@ def test_r128n6_edge_windows_fixture_vs_oracle(m):
         tops, valid, digest = o.sweep(s, s, 6, w["rank_begin"], w["rank_end"], objs, w["K"], RP, 2, 4, keys=keys)
         assert valid == c["valid"] and str(digest) == c["digest"]
         assert [[[str(k), r] for k, r in t] for t in tops] == c["tops"]
+
+
+def _around_pin():
+    path = os.path.join(G, "syn_r128n6_around_pin.json")
+    if not os.path.exists(path):
+        pytest.skip("syn_r128n6_around_pin.json not generated yet (tests/golden/make_keys_golden.py around)")
+    return json.load(open(path)), json.load(open(os.path.join(G, "syn_r128n6_pin.json")))
+
+
+def test_r128n6_pin_records_in_their_oracle_neighbourhoods():
+    """Config 5's full-size pin (GPU: group == generic) against the oracle
+    around its own records (syn_r128n6_around_pin.json): the oracle sweeps
+    2 x 2,048 colex ranks around each of the 800 reported records, so
+      * every reported record is among its window's 100 best in the oracle's
+        own sweep, with the same key (its key and standing are the oracle's,
+        not only its order among the reported records);
+      * no config of those windows at or below an objective's 100th reported
+        (key, rank) is missing from the pin (the records' closest colex
+        neighbours, which share at least 3 of the 6 members, do not beat
+        them unreported)."""
+    fx, pin = _around_pin()
+    assert fx["K"] == pin["K"] == 100 and fx["objectives"] == pin["objectives"]
+    wins = fx["windows"]
+    found = 0
+    for o, t in enumerate(pin["tops"]):
+        recs = [(int(k), r) for k, r in t]
+        kth, S = recs[-1], set(recs)
+        for key, rank in recs:
+            w = next(w for w in wins if w["rank_begin"] <= rank < w["rank_end"])
+            lst = [(int(k), r) for k, r in w["tops"][o]]
+            assert (key, rank) in lst, (o, rank)
+            found += 1
+        for w in wins:
+            lst = [(int(k), r) for k, r in w["tops"][o]]
+            assert all(rec in S for rec in lst if rec <= kth), (o, w["rank_begin"])
+            # the fixture keeps every list up to one record past the K-th; a
+            # window whose whole K=100 list is at or below it must end on the
+            # K-th itself (objective 7's 100 records are 100 consecutive ranks
+            # of one key), or configs would be left unchecked
+            if w["full_below_kth"][o]:
+                assert lst[-1] == kth, (o, w["rank_begin"])
+    assert found == 800
+
+
+@pytest.mark.parametrize("i", [0, 269, 537])
+def test_r128n6_around_pin_fixture_vs_oracle(i):
+    """Three of the around-pin windows swept again by the oracle here."""
+    from fantoch_amd import _lib
+    from fantoch_amd.bote import CONFIG5_OBJECTIVES
+
+    fx, _ = _around_pin()
+    w = fx["windows"][i]
+    p = Planet.synthetic(128)
+    o = O.OraclePlanet.of(p)
+    s = np.arange(128, dtype=np.uint32)
+    tops, valid, digest = o.sweep(s, s, 6, w["rank_begin"], w["rank_end"], list(CONFIG5_OBJECTIVES), fx["K"], RP, 2, 4,
+                                  keys=_lib.KEYS_TEMPO_ALL_LEADERS)
+    assert valid == w["valid"] and str(digest) == w["digest"]
+    assert [[[str(k), r] for k, r in t][:len(s_)] for t, s_ in zip(tops, w["tops"])] == w["tops"]
