@@ -522,14 +522,6 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
   tk.tmp = (Rec*)(smem + off[11]);
   tk.thr = (Rec*)(smem + off[12]);
   const uint32_t thra = LB + (uint32_t)off[12];  // (the thresholds' LDS address)
-  // the screens' bounds (lock[1], lock[2]), which other waves lower: a
-  // relaxed LDS atomic load each step (a volatile read through the generic
-  // `lock` pointer compiled to a flat load behind a full vmcnt + lgkmcnt wait,
-  // its address rebuilt from two spilled SGPRs)
-  const uint32_t locka = LB + (uint32_t)off[13];
-  auto lock_ld = [&](uint32_t i) {
-    return __hip_atomic_load((AS3 int*)(uintptr_t)(locka + 4 * i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  };
   tk.cnt = nullptr;
   int* lock = (int*)(smem + off[13]);
   const uint32_t tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, BD = blockDim.x, WPB = BD >> 6;
@@ -1900,7 +1892,7 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
                     T += (int32_t)(uint32_t)mom[f == 1 ? SLOT_FF1 : SLOT_FF2].s1 - a1 +
                          30 * ((int32_t)(uint32_t)mom[SLOT_E].s1 - a1);
                   }
-                  const bool maybe = T >= lock_ld(1);  // (score_tlo)
+                  const bool maybe = T >= *(volatile int*)(lock + 1);  // (score_tlo)
                   PSTAT(a, 9, maybe);  // f64 score
                   if (maybe) {
                     double score = 0.0;
@@ -1926,7 +1918,7 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
                   // cross-multiplied, the threshold's f32 bound from LDS
                   // (cov_tf32; +inf, or a NaN key: every config passes)
                   const float S = (float)(uint32_t)m.s1;
-                  const bool maybe = !(va1 > __int_as_float(lock_ld(2)) * (S * S));
+                  const bool maybe = !(va1 > __int_as_float(*(volatile int*)(lock + 2)) * (S * S));
                   PSTAT(a, 10, maybe);  // COV af1 key (f64)
                   if (maybe) {
                     ok[3] = true;
@@ -1958,7 +1950,7 @@ __global__ void __launch_bounds__(XK ? GROUP_XK_MAX_BD : GROUP_MAX_BD,
                                  (uint32_t)__shfl_xor((int)(uint32_t)v, d);
               v = w < v ? w : v;
             }
-            uint32_t ch = chunk;
+            uint32_t ch = uni(chunk);
             // (an opaque copy: the compiler hoisted these 8 slot addresses out
             // of the step loop into the chunk head, where the register-bound
             // XK kernel spilled them -- 4 KB of scratch writes per chunk of the
@@ -2131,6 +2123,8 @@ static const void* group_fn(const FastArgs& a, uint32_t n, bool def) {
     FN_CASE(7)
 #elif defined(BOTE_ISA_N6)
     FN_CASE(6)
+#elif defined(BOTE_ISA_N5)
+    FN_CASE(5)
 #else
     FN_CASE(4) FN_CASE(5) FN_CASE(6) FN_CASE(7) FN_CASE0(8) FN_CASE0(9) FN_CASE0(10) FN_CASE0(11) FN_CASE0(12)
     FN_CASE0(13) FN_CASE0(14) FN_CASE0(15) FN_CASE0(16)
@@ -2161,6 +2155,8 @@ hipError_t launch_group(const FastArgs& a, uint32_t n, bool def, uint32_t grid, 
     GS_CASE(7)
 #elif defined(BOTE_ISA_N6)  // (the n = 6 kernels: BASELINE config 5)
     GS_CASE(6)
+#elif defined(BOTE_ISA_N5)
+    GS_CASE(5)
 #else
     GS_CASE(4) GS_CASE(5) GS_CASE(6) GS_CASE(7) GS_CASE0(8) GS_CASE0(9) GS_CASE0(10) GS_CASE0(11) GS_CASE0(12)
     GS_CASE0(13) GS_CASE0(14) GS_CASE0(15) GS_CASE0(16)
