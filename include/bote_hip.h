@@ -330,7 +330,12 @@ int bote_sweep_destroy(bote_sweep* s);
  * bote_search_create does all host work once: one sweep, stream and result
  * buffer per shard, the shard bounds (equal estimated cost, as
  * bote_sweep_split) and each shard's work-chunk table, from ONE host walk of
- * the rank space shared by all shards; it returns with the handle idle.
+ * the rank space shared by all shards; it returns with the handle idle.  For
+ * every shard on a device other than planets[0]'s it checks
+ * hipDeviceCanAccessPeer and enables that device's access to planets[0]'s
+ * ("already enabled" is success; a failure to enable returns BOTE_E_DEVICE),
+ * so the shard writes its result block over xGMI; without peer capability the
+ * runtime stages the copy through host memory.
  * bote_search_launch is device work only and asynchronous: every shard's
  * sweep on its own stream, a peer copy of its result block to planets[0]'s
  * device, and a (key, rank) merge tree there.  It may be called repeatedly
