@@ -13,7 +13,10 @@ checks made here:
     oracle's ordered list over the reported configs equals the device's).
 bench.py --workload r128n6 checks its result against this pin and says so.
 
-  python scripts/pin_r128n6.py OUT.json     (on a GPU box)
+  python scripts/pin_r128n6.py OUT.json [--base]     (on a GPU box)
+
+--base: the same for the 10 compute_stats keys and DEFAULT_OBJECTIVES
+(bench.py --workload r128n6_base), pinned as syn_r128n6_base_pin.json.
 """
 import json
 import os
@@ -28,19 +31,21 @@ sys.path.insert(0, os.path.join(ROOT, "oracle"))
 
 import oracle as O  # noqa: E402
 from fantoch_amd import _lib  # noqa: E402
-from fantoch_amd.bote import CONFIG5_OBJECTIVES, DEFAULT_RANKING, DevicePlanet, Sweep  # noqa: E402
+from fantoch_amd.bote import CONFIG5_OBJECTIVES, DEFAULT_OBJECTIVES, DEFAULT_RANKING, DevicePlanet, Sweep  # noqa: E402
 from fantoch_amd.planet import Planet  # noqa: E402
 
 
 def main():
     out_path = sys.argv[1]
+    base = "--base" in sys.argv[2:]
+    keys = 0 if base else _lib.KEYS_TEMPO_ALL_LEADERS
+    objectives = DEFAULT_OBJECTIVES if base else CONFIG5_OBJECTIVES
     p = Planet.synthetic(128)
     dp = DevicePlanet(p)
     srv = np.arange(128, dtype=np.uint32)
     res = {}
     for k in ("group", "generic"):
-        sw = Sweep(dp, srv, srv, 6, CONFIG5_OBJECTIVES, K=100, ranking=DEFAULT_RANKING, digest=True, kernel=k,
-                   keys=_lib.KEYS_TEMPO_ALL_LEADERS)
+        sw = Sweep(dp, srv, srv, 6, objectives, K=100, ranking=DEFAULT_RANKING, digest=True, kernel=k, keys=keys)
         assert sw.kernel_path() == k
         t0 = time.time()
         sw.launch(0, sw.total)
@@ -54,20 +59,22 @@ def main():
     o = O.OraclePlanet.of(p)
     rp = (DEFAULT_RANKING.min_mean_fpaxos_improv, DEFAULT_RANKING.min_mean_epaxos_improv,
           DEFAULT_RANKING.min_fairness_fpaxos_improv, DEFAULT_RANKING.min_mean_decrease)
-    for oi, obj in enumerate(CONFIG5_OBJECTIVES):
+    for oi, obj in enumerate(objectives):
         recs = tops[oi]
         t, _, _ = o.sweep_ranks(srv, srv, 6, [rk for _, rk in recs], [obj], 100, rp, DEFAULT_RANKING.ft_metric.value,
-                                threads=16, keys=1)
+                                threads=16, keys=1 if keys else 0)
         if [(int(k), int(rk)) for k, rk in t[0]] != recs:
             sys.exit(f"objective {oi}: the oracle's re-derivation differs: no pin")
     pin = {
         "what": ("regression pin of BASELINE config 5 at full size: synthetic R=128 planet (seed 0x5EED0128), n=6, "
-                 "all 5,423,611,200 configs, extended key set (BOTE_KEYS_TEMPO_ALL_LEADERS), CONFIG5_OBJECTIVES, "
-                 "K=100, RankingParams(110,35,0,15,F1F2)"),
+                 "all 5,423,611,200 configs, " +
+                 ("the 10 compute_stats keys, DEFAULT_OBJECTIVES" if base else
+                  "extended key set (BOTE_KEYS_TEMPO_ALL_LEADERS), CONFIG5_OBJECTIVES") +
+                 ", K=100, RankingParams(110,35,0,15,F1F2)"),
         "source": ("GPU, NOT the oracle: the group kernel equals the exact generic kernel at full size, and every "
                    "reported record was re-derived by the oracle (keys and order); generator scripts/pin_r128n6.py"),
-        "R": 128, "n": 6, "rank_begin": 0, "rank_end": total, "keys": 1, "K": 100,
-        "objectives": [list(x) for x in CONFIG5_OBJECTIVES],
+        "R": 128, "n": 6, "rank_begin": 0, "rank_end": total, "keys": 0 if base else 1, "K": 100,
+        "objectives": [list(x) for x in objectives],
         "valid": valid, "digest": str(digest), "tops": [[[str(k), rk] for k, rk in t] for t in tops],
     }
     os.makedirs(os.path.dirname(os.path.abspath(out_path)), exist_ok=True)
