@@ -4,7 +4,7 @@ BOTE_KEYS_TEMPO_ALL_LEADERS) and the random R=128 n=6 windows, from the CPU
 oracle (oracle/bote_oracle.cpp compute_stats_x, checked against the oracle's
 reference-pinned single calls by tests/test_keys_oracle.py).
 
-  python tests/golden/make_keys_golden.py [--threads T] [topk|windows|edges|around|all]
+  python tests/golden/make_keys_golden.py [--threads T] [topk|windows|edges|around|around_base|all]
 
 Writes:
   topk_x.json   every GCP R20C20 config of n = 2..13 and the synthetic
@@ -30,6 +30,8 @@ Writes:
                 merged, swept with the extended key set (CONFIG5_OBJECTIVES,
                 K=100): the oracle's view of the pin's records and of their
                 colex neighbours
+  syn_r128n6_base_around_pin.json  (round 6) the same around the 10-key
+                pin (syn_r128n6_base_pin.json: DEFAULT_OBJECTIVES, 5 x 100)
 Resumable: finished windows are kept in oracle/build/keys_windows.jsonl
 (edges: oracle/build/keys_edges.jsonl; around: keys_around.jsonl).
 
@@ -193,10 +195,10 @@ A_P = 2_048  # the windows around the pin's records: ranks on each side
 KEEP_A = 8  # records kept per window list at least
 
 
-def around_windows():
-    """[rank - A_P, rank + A_P) around every record of syn_r128n6_pin.json
-    (8 objectives x 100), clipped to the rank space, overlapping ones merged."""
-    pin = json.load(open(os.path.join(HERE, "syn_r128n6_pin.json")))
+def around_windows(pin_name="syn_r128n6_pin.json"):
+    """[rank - A_P, rank + A_P) around every record of a pin (syn_r128n6_pin.json:
+    8 objectives x 100), clipped to the rank space, overlapping ones merged."""
+    pin = json.load(open(os.path.join(HERE, pin_name)))
     total = comb(128, 6)
     iv = sorted((max(0, r - A_P), min(total, r + A_P)) for t in pin["tops"] for _, r in t)
     out = []
@@ -208,21 +210,24 @@ def around_windows():
     return [tuple(x) for x in out]
 
 
-def make_around(threads):
+def make_around(threads, base=False):
+    """base: the 10-key pin (syn_r128n6_base_pin.json), DEFAULT_OBJECTIVES."""
+    pin_name = "syn_r128n6_base_pin.json" if base else "syn_r128n6_pin.json"
+    objs, keys = (DEFAULT_OBJECTIVES, 0) if base else (objectives_x(6), 1)
     p = Planet.synthetic(128)
-    scratch = os.path.join(ROOT, "oracle", "build", "keys_around.jsonl")
+    scratch = os.path.join(ROOT, "oracle", "build", "keys_around_base.jsonl" if base else "keys_around.jsonl")
     os.makedirs(os.path.dirname(scratch), exist_ok=True)
     done = {}
     if os.path.exists(scratch):
         for line in open(scratch):
             w = json.loads(line)
             done[(w["rank_begin"], w["rank_end"])] = w
-    jobs = around_windows()
+    jobs = around_windows(pin_name)
     t_all = time.time()
     for b, e in jobs:
         if (b, e) in done:
             continue
-        x = sweep_case(p, 6, b, e, objectives_x(6), 100, 1, threads)
+        x = sweep_case(p, 6, b, e, objs, 100, keys, threads)
         w = dict(rank_begin=b, rank_end=e, **x)
         with open(scratch, "a") as fh:
             fh.write(json.dumps(w) + "\n")
@@ -233,7 +238,7 @@ def make_around(threads):
     # (key, rank) of the objective, and at least KEEP_A records: every window
     # config at or below that record is kept, and the rest of a K=100 list is
     # prefix-checked on the GPU
-    pin = json.load(open(os.path.join(HERE, "syn_r128n6_pin.json")))
+    pin = json.load(open(os.path.join(HERE, pin_name)))
     kth = [(int(t[-1][0]), t[-1][1]) for t in pin["tops"]]
     wins = []
     for b, e in jobs:
@@ -245,21 +250,25 @@ def make_around(threads):
             tops.append(t[:max(KEEP_A, below + 1)])
         w["tops"], w["full_below_kth"] = tops, full
         wins.append(w)
-    d = {"what": ("oracle sweeps (extended key set, CONFIG5_OBJECTIVES, K=100, RankingParams(110,35,0,15,F1F2)) of "
+    d = {"what": ("oracle sweeps (%s, K=100, RankingParams(110,35,0,15,F1F2)) of "
                   "the synthetic R=128 planet, n=6, over a window of %d ranks on each side of every record of "
-                  "syn_r128n6_pin.json (8 objectives x 100 records; overlapping windows merged): the pin's "
+                  "%s (%d objectives x 100 records; overlapping windows merged): the pin's "
                   "records and their colex neighbours, where their closest competitors are.  Each objective's "
                   "K=100 list is kept up to one record past the pin's 100th (key, rank) and at least %d records "
-                  "(a prefix of the oracle's list)" % (A_P, KEEP_A)),
-         "generator": "tests/golden/make_keys_golden.py around",
-         "R": 128, "n": 6, "keys": 1, "K": 100, "objectives": [list(o) for o in objectives_x(6)],
+                  "(a prefix of the oracle's list)" % (
+                      "the 10 compute_stats keys, DEFAULT_OBJECTIVES" if base else
+                      "extended key set, CONFIG5_OBJECTIVES", A_P, pin_name, len(objs), KEEP_A)),
+         "generator": "tests/golden/make_keys_golden.py " + ("around_base" if base else "around"),
+         "R": 128, "n": 6, "keys": keys, "K": 100, "objectives": [list(o) for o in objs], "pin": pin_name,
          "windows": wins}
-    json.dump(d, open(os.path.join(HERE, "syn_r128n6_around_pin.json"), "w"))
+    json.dump(d, open(os.path.join(HERE, "syn_r128n6_base_around_pin.json" if base else "syn_r128n6_around_pin.json"),
+                      "w"))
 
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("what", nargs="?", default="all", choices=["topk", "windows", "edges", "around", "all"])
+    ap.add_argument("what", nargs="?", default="all", choices=["topk", "windows", "edges", "around", "around_base",
+                                                                 "all"])
     ap.add_argument("--threads", type=int, default=8)
     a = ap.parse_args()
     if a.what in ("topk", "all"):
@@ -270,6 +279,8 @@ def main():
         make_edges(a.threads)
     if a.what in ("around", "all"):
         make_around(a.threads)
+    if a.what in ("around_base", "all"):
+        make_around(a.threads, base=True)
 
 
 if __name__ == "__main__":

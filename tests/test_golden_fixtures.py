@@ -107,14 +107,20 @@ def test_r128n6_edge_windows_fixture_vs_oracle(m):
         assert [[[str(k), r] for k, r in t] for t in tops] == c["tops"]
 
 
-def _around_pin():
-    path = os.path.join(G, "syn_r128n6_around_pin.json")
+AROUND = {"x": ("syn_r128n6_around_pin.json", "syn_r128n6_pin.json"),
+          "base": ("syn_r128n6_base_around_pin.json", "syn_r128n6_base_pin.json")}
+
+
+def _around_pin(kind="x"):
+    fx_name, pin_name = AROUND[kind]
+    path = os.path.join(G, fx_name)
     if not os.path.exists(path):
-        pytest.skip("syn_r128n6_around_pin.json not generated yet (tests/golden/make_keys_golden.py around)")
-    return json.load(open(path)), json.load(open(os.path.join(G, "syn_r128n6_pin.json")))
+        pytest.skip(f"{fx_name} not generated yet (tests/golden/make_keys_golden.py around)")
+    return json.load(open(path)), json.load(open(os.path.join(G, pin_name)))
 
 
-def test_r128n6_pin_records_in_their_oracle_neighbourhoods():
+@pytest.mark.parametrize("kind", ["x", "base"])
+def test_r128n6_pin_records_in_their_oracle_neighbourhoods(kind):
     """Config 5's full-size pin (GPU: group == generic) against the oracle
     around its own records (syn_r128n6_around_pin.json): the oracle sweeps
     2 x 2,048 colex ranks around each of the 800 reported records, so
@@ -125,7 +131,7 @@ def test_r128n6_pin_records_in_their_oracle_neighbourhoods():
         (key, rank) is missing from the pin (the records' closest colex
         neighbours, which share at least 3 of the 6 members, do not beat
         them unreported)."""
-    fx, pin = _around_pin()
+    fx, pin = _around_pin(kind)
     assert fx["K"] == pin["K"] == 100 and fx["objectives"] == pin["objectives"]
     wins = fx["windows"]
     found = 0
@@ -146,21 +152,18 @@ def test_r128n6_pin_records_in_their_oracle_neighbourhoods():
             # of one key), or configs would be left unchecked
             if w["full_below_kth"][o]:
                 assert lst[-1] == kth, (o, w["rank_begin"])
-    assert found == 800
+    assert found == 100 * len(pin["tops"])
 
 
-@pytest.mark.parametrize("i", [0, 269, 537])
-def test_r128n6_around_pin_fixture_vs_oracle(i):
-    """Three of the around-pin windows swept again by the oracle here."""
-    from fantoch_amd import _lib
-    from fantoch_amd.bote import CONFIG5_OBJECTIVES
-
-    fx, _ = _around_pin()
+@pytest.mark.parametrize("kind,i", [("x", 0), ("x", 269), ("x", 537), ("base", 0), ("base", 371)])
+def test_r128n6_around_pin_fixture_vs_oracle(kind, i):
+    """Some of the around-pin windows swept again by the oracle here."""
+    fx, _ = _around_pin(kind)
     w = fx["windows"][i]
     p = Planet.synthetic(128)
     o = O.OraclePlanet.of(p)
     s = np.arange(128, dtype=np.uint32)
-    tops, valid, digest = o.sweep(s, s, 6, w["rank_begin"], w["rank_end"], list(CONFIG5_OBJECTIVES), fx["K"], RP, 2, 4,
-                                  keys=_lib.KEYS_TEMPO_ALL_LEADERS)
+    objs = [tuple(x) for x in fx["objectives"]]
+    tops, valid, digest = o.sweep(s, s, 6, w["rank_begin"], w["rank_end"], objs, fx["K"], RP, 2, 4, keys=fx["keys"])
     assert valid == w["valid"] and str(digest) == w["digest"]
     assert [[[str(k), r] for k, r in t][:len(s_)] for t, s_ in zip(tops, w["tops"])] == w["tops"]

@@ -286,21 +286,24 @@ def test_r128n6_every_colex_boundary_vs_oracle():
             assert [[[str(k), rk] for k, rk in lst] for lst in r.tops] == c["tops"], (keys, w["m"])
 
 
-def test_r128n6_windows_around_the_pin_vs_oracle():
+@pytest.mark.parametrize("fx_name", ["syn_r128n6_around_pin.json", "syn_r128n6_base_around_pin.json"])
+def test_r128n6_windows_around_the_pin_vs_oracle(fx_name):
     """The oracle's windows of 2 x 2,048 ranks around every record of config
-    5's full-size regression pin (tests/golden/syn_r128n6_around_pin.json, 538
-    merged windows, 2.3e6 configs), swept by the group kernel with the
-    extended key set: valid count, digest and every objective's top-100 equal
+    5's full-size regression pins (tests/golden/syn_r128n6_around_pin.json,
+    538 merged windows, 2.3e6 configs, extended keys; and
+    syn_r128n6_base_around_pin.json, the 10 compute_stats keys), swept by the
+    group kernel with the pin's key set: valid count, digest and every objective's top-100 equal
     the oracle's (each list up to one record past the pin's 100th, as the
     fixture keeps it)."""
-    fx = _fixture("syn_r128n6_around_pin.json")
+    fx = _fixture(fx_name)
     p = Planet.synthetic(128)
     dp = DevicePlanet(p)
     srv = np.arange(128, dtype=np.uint32)
-    sw = Sweep(dp, srv, srv, 6, CONFIG5_OBJECTIVES, K=fx["K"], ranking=DEFAULT_RANKING, digest=True,
-               keys=_lib.KEYS_TEMPO_ALL_LEADERS)
+    objs = CONFIG5_OBJECTIVES if fx["keys"] else DEFAULT_OBJECTIVES
+    sw = Sweep(dp, srv, srv, 6, objs, K=fx["K"], ranking=DEFAULT_RANKING, digest=True,
+               keys=_lib.KEYS_TEMPO_ALL_LEADERS if fx["keys"] else 0)
     assert sw.kernel_path() == "group"
-    assert [tuple(o) for o in fx["objectives"]] == list(CONFIG5_OBJECTIVES)
+    assert [tuple(o) for o in fx["objectives"]] == list(objs)
     for w in fx["windows"]:
         sw.launch(w["rank_begin"], w["rank_end"])
         r = sw.result()
