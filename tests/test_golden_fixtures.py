@@ -167,3 +167,32 @@ def test_r128n6_around_pin_fixture_vs_oracle(kind, i):
     tops, valid, digest = o.sweep(s, s, 6, w["rank_begin"], w["rank_end"], objs, fx["K"], RP, 2, 4, keys=fx["keys"])
     assert valid == w["valid"] and str(digest) == w["digest"]
     assert [[[str(k), r] for k, r in t][:len(s_)] for t, s_ in zip(tops, w["tops"])] == w["tops"]
+
+
+def test_r128n6_oracle_range_agrees_with_the_base_pin():
+    """The oracle's contiguous 10-key range of config 5
+    (syn_r128n6_1700000000_1800663296.json, 1.0e8 configs) against the GPU's
+    full-size 10-key pin (syn_r128n6_base_pin.json): every pin record inside
+    the range is in the oracle's range list (when at or below the list's
+    100th), and every record of the oracle's list at or below the pin's 100th
+    is in the pin."""
+    path = os.path.join(G, "syn_r128n6_1700000000_1800663296.json")
+    if not os.path.exists(path):
+        pytest.skip("oracle range fixture not generated")
+    fx = json.load(open(path))
+    pin = json.load(open(os.path.join(G, "syn_r128n6_base_pin.json")))
+    assert fx["objectives"] == pin["objectives"] and fx["K"] == pin["K"]
+    rb, re_ = fx["rank_begin"], fx["rank_end"]
+    inside = 0
+    for o, t in enumerate(pin["tops"]):
+        recs = [(int(k), r) for k, r in t]
+        lst = [tuple(x) for x in fx["tops"][o]]
+        kth, last = recs[-1], lst[-1]
+        for rec in recs:
+            if rb <= rec[1] < re_ and rec <= last:
+                assert rec in lst, (o, rec)
+                inside += 1
+        for rec in lst:
+            if rec <= kth:
+                assert rec in recs, (o, rec)
+    print("pin records inside the oracle range:", inside)

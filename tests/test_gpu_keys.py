@@ -311,3 +311,22 @@ def test_r128n6_windows_around_the_pin_vs_oracle(fx_name):
         # (the fixture keeps each list up to one record past the pin's K-th: a prefix)
         assert [[[str(k), rk] for k, rk in lst][:len(s)] for lst, s in zip(r.tops, w["tops"])] == w["tops"], \
             w["rank_begin"]
+
+
+def test_r128n6_contiguous_oracle_range():
+    """BASELINE config 5's 10-key sweep over 100,663,296 consecutive colex
+    ranks [1.7e9, 1,800,663,296) that the CPU oracle swept in full
+    (tests/golden/syn_r128n6_1700000000_1800663296.json,
+    scripts/oracle_full_sweep.py on a GPU box's 16 CPUs, 1e5 configs/s): the
+    group kernel's valid count, digest and 5 x 100 top-K equal the oracle's."""
+    fx = _fixture("syn_r128n6_1700000000_1800663296.json")
+    p = Planet.synthetic(128)
+    dp = DevicePlanet(p)
+    srv = np.arange(128, dtype=np.uint32)
+    sw = Sweep(dp, srv, srv, 6, DEFAULT_OBJECTIVES, K=fx["K"], ranking=DEFAULT_RANKING, digest=True)
+    assert sw.kernel_path() == "group"
+    assert [tuple(o) for o in fx["objectives"]] == list(DEFAULT_OBJECTIVES)
+    sw.launch(fx["rank_begin"], fx["rank_end"])
+    r = sw.result()
+    assert (r.valid, r.digest) == (fx["valid"], fx["digest"])
+    assert [[[int(k), int(rk)] for k, rk in lst] for lst in r.tops] == fx["tops"]
