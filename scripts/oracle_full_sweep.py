@@ -69,15 +69,21 @@ def main():
     ap.add_argument("--sweep-begin", type=int, default=None, help="first chunk to sweep (chunk-aligned)")
     ap.add_argument("--sweep-end", type=int, default=None, help="stop before this rank (with --partial)")
     ap.add_argument("--time-limit", type=float, default=None, help="stop after this many seconds")
+    ap.add_argument("--keys", type=int, default=0,
+                    help="1: the extended key set (BOTE_KEYS_TEMPO_ALL_LEADERS) with CONFIG5_OBJECTIVES")
     args = ap.parse_args()
 
+    global OBJECTIVES
+    if args.keys:
+        from fantoch_amd.bote import CONFIG5_OBJECTIVES
+        OBJECTIVES = [tuple(o) for o in CONFIG5_OBJECTIVES]
     R, n = WORKLOADS[args.workload]
     planet = Planet.synthetic(R)
     total = binom(R, n)
     rb = args.rank_begin
     re = total if args.rank_end is None else args.rank_end
     name = args.name or (f"syn_{args.workload}_full" if (rb, re) == (0, total) else
-                         f"syn_{args.workload}_{rb}_{re}")
+                         f"syn_{args.workload}{'_x' if args.keys else ''}_{rb}_{re}")
     state = args.state or os.path.join(ROOT, "oracle", "build", f"{name}_chunks.jsonl")
     os.makedirs(os.path.dirname(state), exist_ok=True)
     done = {}
@@ -105,7 +111,8 @@ def main():
                 print(f"[{name}] time limit reached at rank {b}", flush=True)
                 break
             t0 = time.time()
-            tops, valid, digest = o.sweep(srv, srv, n, b, e, OBJECTIVES, args.K, RPARAMS, FT_F1F2, args.threads)
+            tops, valid, digest = o.sweep(srv, srv, n, b, e, OBJECTIVES, args.K, RPARAMS, FT_F1F2, args.threads,
+                                          keys=args.keys)
             d = {"begin": b, "end": e, "valid": valid, "digest": digest,
                  "tops": [[[int(k), int(r)] for k, r in t] for t in tops], "seconds": time.time() - t0}
             fh.write(json.dumps(d) + "\n")
@@ -125,8 +132,8 @@ def main():
         "what": f"oracle (oracle/bote_oracle.cpp oracle_sweep) over colex ranks [{rb}, {re}) of the synthetic "
                 f"R={R} planet (Planet.synthetic), n={n}, clients = all R regions + colocated",
         "generator": "scripts/oracle_full_sweep.py",
-        "R": R, "n": n, "rank_begin": rb, "rank_end": re, "K": args.K,
-        "objectives": OBJECTIVES, "ranking": list(RPARAMS), "ft_metric": FT_F1F2,
+        "R": R, "n": n, "rank_begin": rb, "rank_end": re, "K": args.K, "keys": args.keys,
+        "objectives": [list(o) for o in OBJECTIVES], "ranking": list(RPARAMS), "ft_metric": FT_F1F2,
         "valid": sum(p["valid"] for p in parts),
         "digest": sum(p["digest"] for p in parts) % (1 << 64),
         "tops": merge_tops([p["tops"] for p in parts], args.K),

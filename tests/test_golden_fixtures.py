@@ -171,12 +171,12 @@ def test_r128n6_around_pin_fixture_vs_oracle(kind, i):
 
 def test_r128n6_oracle_range_agrees_with_the_base_pin():
     """The oracle's contiguous 10-key range of config 5
-    (syn_r128n6_1700000000_1800663296.json, 1.0e8 configs) against the GPU's
+    (syn_r128n6_1700000000_1897132288.json, 2.0e8 configs) against the GPU's
     full-size 10-key pin (syn_r128n6_base_pin.json): every pin record inside
     the range is in the oracle's range list (when at or below the list's
     100th), and every record of the oracle's list at or below the pin's 100th
     is in the pin."""
-    path = os.path.join(G, "syn_r128n6_1700000000_1800663296.json")
+    path = os.path.join(G, "syn_r128n6_1700000000_1897132288.json")
     if not os.path.exists(path):
         pytest.skip("oracle range fixture not generated")
     fx = json.load(open(path))

@@ -314,12 +314,12 @@ def test_r128n6_windows_around_the_pin_vs_oracle(fx_name):
 
 
 def test_r128n6_contiguous_oracle_range():
-    """BASELINE config 5's 10-key sweep over 100,663,296 consecutive colex
-    ranks [1.7e9, 1,800,663,296) that the CPU oracle swept in full
-    (tests/golden/syn_r128n6_1700000000_1800663296.json,
+    """BASELINE config 5's 10-key sweep over 197,132,288 consecutive colex
+    ranks [1.7e9, 1,897,132,288) that the CPU oracle swept in full
+    (tests/golden/syn_r128n6_1700000000_1897132288.json,
     scripts/oracle_full_sweep.py on a GPU box's 16 CPUs, 1e5 configs/s): the
     group kernel's valid count, digest and 5 x 100 top-K equal the oracle's."""
-    fx = _fixture("syn_r128n6_1700000000_1800663296.json")
+    fx = _fixture("syn_r128n6_1700000000_1897132288.json")
     p = Planet.synthetic(128)
     dp = DevicePlanet(p)
     srv = np.arange(128, dtype=np.uint32)
