@@ -313,19 +313,25 @@ def test_r128n6_windows_around_the_pin_vs_oracle(fx_name):
             w["rank_begin"]
 
 
-def test_r128n6_contiguous_oracle_range():
-    """BASELINE config 5's 10-key sweep over 197,132,288 consecutive colex
-    ranks [1.7e9, 1,897,132,288) that the CPU oracle swept in full
-    (tests/golden/syn_r128n6_1700000000_1897132288.json,
-    scripts/oracle_full_sweep.py on a GPU box's 16 CPUs, 1e5 configs/s): the
-    group kernel's valid count, digest and 5 x 100 top-K equal the oracle's."""
-    fx = _fixture("syn_r128n6_1700000000_1897132288.json")
+@pytest.mark.parametrize("fx_name", ["syn_r128n6_1700000000_1897132288.json", "syn_r128n6_x_2005000000_2035408704.json"])
+def test_r128n6_contiguous_oracle_range(fx_name):
+    """BASELINE config 5 over consecutive colex ranks that the CPU oracle swept
+    in full (scripts/oracle_full_sweep.py on a GPU box's 16 CPUs): the 10-key
+    sweep over 197,132,288 ranks [1.7e9, 1,897,132,288), and config 5 as
+    stated (the extended keys, 8 objectives) over 30,408,704 ranks
+    [2,005,000,000, 2,035,408,704), which hold the pin's 100 records of
+    objective 7 (100 consecutive ranks of one key).  The group kernel's valid
+    count, digest and top-100 lists equal the oracle's."""
+    fx = _fixture(fx_name)
     p = Planet.synthetic(128)
     dp = DevicePlanet(p)
     srv = np.arange(128, dtype=np.uint32)
-    sw = Sweep(dp, srv, srv, 6, DEFAULT_OBJECTIVES, K=fx["K"], ranking=DEFAULT_RANKING, digest=True)
+    keys = fx.get("keys", 0)
+    objs = CONFIG5_OBJECTIVES if keys else DEFAULT_OBJECTIVES
+    sw = Sweep(dp, srv, srv, 6, objs, K=fx["K"], ranking=DEFAULT_RANKING, digest=True,
+               keys=_lib.KEYS_TEMPO_ALL_LEADERS if keys else 0)
     assert sw.kernel_path() == "group"
-    assert [tuple(o) for o in fx["objectives"]] == list(DEFAULT_OBJECTIVES)
+    assert [tuple(o) for o in fx["objectives"]] == list(objs)
     sw.launch(fx["rank_begin"], fx["rank_end"])
     r = sw.result()
     assert (r.valid, r.digest) == (fx["valid"], fx["digest"])
