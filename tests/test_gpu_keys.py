@@ -313,14 +313,16 @@ def test_r128n6_windows_around_the_pin_vs_oracle(fx_name):
             w["rank_begin"]
 
 
-@pytest.mark.parametrize("fx_name", ["syn_r128n6_1700000000_1897132288.json", "syn_r128n6_x_2005000000_2035408704.json"])
+@pytest.mark.parametrize("fx_name", ["syn_r128n6_1700000000_1897132288.json", "syn_r128n6_x_2005000000_2035408704.json",
+                                     "syn_r128n6_x_540000000_570408704.json"])
 def test_r128n6_contiguous_oracle_range(fx_name):
     """BASELINE config 5 over consecutive colex ranks that the CPU oracle swept
     in full (scripts/oracle_full_sweep.py on a GPU box's 16 CPUs): the 10-key
     sweep over 197,132,288 ranks [1.7e9, 1,897,132,288), and config 5 as
     stated (the extended keys, 8 objectives) over 30,408,704 ranks
-    [2,005,000,000, 2,035,408,704), which hold the pin's 100 records of
-    objective 7 (100 consecutive ranks of one key).  The group kernel's valid
+    [2,005,000,000, 2,035,408,704) and [540,000,000, 570,408,704), which
+    hold the pin's 100 records of objective 7 (100 consecutive ranks of one
+    key) and of objective 2 (100 ties at one key).  The group kernel's valid
     count, digest and top-100 lists equal the oracle's."""
     fx = _fixture(fx_name)
     p = Planet.synthetic(128)
