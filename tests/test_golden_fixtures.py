@@ -177,7 +177,8 @@ def test_r128n6_around_pin_fixture_vs_oracle(kind, i):
     ("syn_r128n6_x_327000000_356360128.json", "syn_r128n6_pin.json", 20),
     ("syn_r128n6_x_1823000000_1852360128.json", "syn_r128n6_pin.json", 20),
     ("syn_r128n6_x_4963900000_4992211552.json", "syn_r128n6_pin.json", 15),
-    ("syn_r128n6_x_4513400000_4542760128.json", "syn_r128n6_pin.json", 15)])
+    ("syn_r128n6_x_4513400000_4542760128.json", "syn_r128n6_pin.json", 15),
+    ("syn_r128n6_x_2400000000_2429360128.json", "syn_r128n6_pin.json", 15)])
 def test_r128n6_oracle_range_agrees_with_the_pin(fx_name, pin_name, least):
     """The oracle's contiguous ranges of config 5 (the 10-key sweep over
     2.0e8 ranks; the extended keys over five ranges of ~3.0e7 ranks placed on

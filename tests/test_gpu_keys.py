@@ -316,7 +316,8 @@ def test_r128n6_windows_around_the_pin_vs_oracle(fx_name):
 @pytest.mark.parametrize("fx_name", ["syn_r128n6_1700000000_1897132288.json", "syn_r128n6_x_2005000000_2035408704.json",
                                      "syn_r128n6_x_540000000_570408704.json", "syn_r128n6_x_1026000000_1056408704.json",
                                      "syn_r128n6_x_327000000_356360128.json", "syn_r128n6_x_1823000000_1852360128.json",
-                                     "syn_r128n6_x_4963900000_4992211552.json", "syn_r128n6_x_4513400000_4542760128.json"])
+                                     "syn_r128n6_x_4963900000_4992211552.json", "syn_r128n6_x_4513400000_4542760128.json",
+                                     "syn_r128n6_x_2400000000_2429360128.json"])
 def test_r128n6_contiguous_oracle_range(fx_name):
     """BASELINE config 5 over consecutive colex ranks that the CPU oracle swept
     in full (scripts/oracle_full_sweep.py on a GPU box's 16 CPUs): the 10-key
